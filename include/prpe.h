@@ -1,0 +1,186 @@
+/*
+ * prpe.h — C ABI of the MI355X-native per-frame inference hot path of the
+ * Person-Recognition-for-Pose-Estimation combined multi-task model.
+ *
+ * The reference (100 % Python, /root/reference) has no native boundary: its device work
+ * is PyTorch/cuDNN operators called from nn.Modules. These entry points
+ * are what a ctypes/FFI binding of that path binds; each cites the reference interface
+ * (file:line) whose arithmetic it replaces. The Python host side
+ * (person-recognition-for-pose-estimation_amd/prpe) mirrors the reference module API.
+ *
+ * Rules (all entry points):
+ *   - Every buffer is caller-allocated device memory; the library never allocates.
+ *   - Tensors are strided float32 views: element strides, any layout (NHWC/NCHW/...).
+ *   - Calls are stream-ordered on the given hipStream_t (passed as void*), no implicit
+ *     synchronisation; safe to call concurrently on different streams/devices.
+ *   - Return 0 on success, a negative errno-style code (-22 = EINVAL) for bad
+ *     arguments (checked before any launch), or a positive hipError_t from the launch.
+ *   - Nothing throws across the ABI.
+ */
+#ifndef PRPE_H_
+#define PRPE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PRPE_ABI_VERSION 1
+
+/* activations (epilogues/prologues) */
+enum prpe_act {
+  PRPE_ACT_NONE = 0,
+  PRPE_ACT_RELU = 1,   /* torch.nn.ReLU */
+  PRPE_ACT_SILU = 2,   /* torch.nn.SiLU  (yolopt/nets/nn.py:28-36) */
+  PRPE_ACT_PRELU = 3,  /* torch.nn.PReLU, per-channel slope (libs/net_adaface.py:153-160) */
+  PRPE_ACT_GELU = 4,   /* exact erf GELU (modify_models.py:356, ViT MLP) */
+  PRPE_ACT_SIGMOID = 5
+};
+
+/* residual modes of the conv epilogue */
+enum prpe_res_mode {
+  PRPE_RES_NONE = 0,
+  PRPE_RES_PRE_ACT = 1,  /* y = act(acc*scale + bias + r)   ResNet bottleneck / IR unit / ViT */
+  PRPE_RES_POST_ACT = 2  /* y = act(acc*scale + bias) + r   yolopt Residual (nn.py:48-49) */
+};
+
+/* A strided 4-D float32 view, logical shape [n, h, w, c]. */
+typedef struct prpe_view {
+  float* ptr;
+  int32_t n, h, w, c;
+  int64_t sn, sh, sw, sc;
+} prpe_view;
+
+/*
+ * Convolution (groups = 1) as an implicit GEMM on MFMA with split-bf16 operands
+ * (fp32 accumulate): see ``precision``.
+ *   y[n,oh,ow,co] = EPI( sum_{kh,kw,ci} PRO(x[n, oh*s-p+kh, ow*s-p+kw, ci]) * W[co,kh,kw,ci] )
+ * PRO(v) = v*in_scale[ci] + in_bias[ci] for in-bounds taps, 0 for padding (IR-50 pre-BN,
+ * libs/net_adaface.py:159). EPI = folded BN / bias (scale, bias), residual, activation.
+ * Weights are packed by the host: bf16 planes [co_pad][k_pad], k = (kh*KW+kw)*Ci+ci,
+ * w = plane0 + plane1 + plane2 (RNE splits).
+ * Replaces: torch.nn.Conv2d + BatchNorm2d (+act, +residual) in training/modify_models.py,
+ * yolopt/nets/nn.py:28-39, libs/net_adaface.py:144-167, torchvision resnet50 (:446),
+ * nn.Linear in ViTPose and IR-50 output_layer (as a 1x1 / 7x7 "conv").
+ */
+typedef struct prpe_conv_desc {
+  prpe_view x;            /* input  [N, Hi, Wi, Ci] */
+  prpe_view y;            /* output [N, Ho, Wo, Co] */
+  prpe_view res;          /* residual [N, Ho, Wo, Co] (ptr may be NULL) */
+  int32_t kh, kw, stride, pad;
+  const uint16_t* w_hi;   /* bf16 bits, plane 0 */
+  const uint16_t* w_lo;   /* plane 1 (precision 0, 2) */
+  const uint16_t* w_lo2;  /* plane 2 (precision 2) */
+  int32_t k_pad, co_pad;  /* packed extents (k_pad % 32 == 0, co_pad % 64 == 0) */
+  const float* scale;     /* [Co] or NULL (= 1) */
+  const float* bias;      /* [Co] or NULL (= 0) */
+  const float* slope;     /* [Co] PReLU slopes or NULL */
+  const float* in_scale;  /* [Ci] or NULL */
+  const float* in_bias;   /* [Ci] or NULL */
+  int32_t act;            /* prpe_act */
+  int32_t res_mode;       /* prpe_res_mode */
+  int32_t precision;      /* 0 = 2-plane split-bf16, 3 MFMA terms (~2^-17);
+                             2 = 3-plane split (exact fp32 operands), 6 terms;
+                             1 = plain bf16 (1 term; diagnostics only) */
+  int32_t tile;           /* 0 = auto */
+} prpe_conv_desc;
+
+int prpe_conv2d(const prpe_conv_desc* d, void* stream);
+
+/*
+ * conv3x3(pad 1) o bilinear-upsample, second stage of the exact algebraic rewrite
+ *   conv3x3(U(x)) = sum_tap shift_tap(U(Z_tap)),   Z_tap = W_tap . x  (low-res 1x1 GEMM)
+ * z: [N, Hi, Wi, 9*Co] low-res per-tap products (channel = tap*Co + co, tap = kh*3+kw).
+ * y[n,oy,ox,co] = act( (sum_tap valid * bilerp(Z_tap, src(oy+kh-1, ox+kw-1))) * scale + bias )
+ * align_corners = 1: src = dst*(in-1)/(out-1);  0: src = max(0,(dst+0.5)*in/out-0.5).
+ * Replaces nn.Upsample(bilinear) + Conv2d(3x3) + BN + act in modify_models.py:47-52,
+ * :237-242, :359-364 and the ViTPose simple decoder (modeling_vitpose.py:120-144).
+ */
+int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,
+                   const float* scale, const float* bias, const float* slope, int32_t act,
+                   void* stream);
+
+/* Depthwise kxk conv (groups = C) + folded BN + act (+ post-act residual add when res.ptr).
+ * Replaces yolopt Conv(g=ch) (nn.py:108, :248-250). */
+int prpe_dwconv(const prpe_view* x, const prpe_view* y, const prpe_view* res,
+                const float* w /* [C][k][k] */, int32_t k, int32_t stride, int32_t pad,
+                const float* scale, const float* bias, int32_t act, void* stream);
+
+/* Max pooling, k x k / stride / pad (-inf padding). torchvision resnet maxpool,
+ * yolopt SPP (nn.py:88-94), IR-50 MaxPool2d(1, s) shortcut (net_adaface.py:148). */
+int prpe_maxpool(const prpe_view* x, const prpe_view* y, int32_t k, int32_t stride,
+                 int32_t pad, void* stream);
+
+/* Nearest x2 upsample (yolopt DarkFPN nn.Upsample(scale_factor=2), nn.py:195). */
+int prpe_upsample_nearest2x(const prpe_view* x, const prpe_view* y, void* stream);
+
+/* Per-sample, per-channel standardisation + sigmoid (modify_models.py:84-86):
+ * y = sigmoid((x - mean_hw) / (std_hw_unbiased + 1e-6)). */
+int prpe_norm_sigmoid(const prpe_view* x, const prpe_view* y, void* stream);
+
+/* LayerNorm over the last dim of rows (ViTPose, eps 1e-12), optional ReLU on the output
+ * (simple decoder's ReLU, modeling_vitpose.py:139). x/y: [rows][C] with row strides. */
+int prpe_layernorm(const float* x, int64_t x_row_stride, float* y, int64_t y_row_stride,
+                   int64_t rows, int32_t C, const float* gamma, const float* beta,
+                   float eps, int32_t relu, void* stream);
+
+/* ViT multi-head self-attention, softmax(Q K^T * scale) V per (frame, head).
+ * qkv: [B*L][3*H*D] rows (q | k | v, head-major inside each), out: [B*L][H*D].
+ * Replaces eager_attention_forward (modeling_vitpose_backbone.py:100-126). */
+int prpe_attention(const float* qkv, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
+                   float scale, void* stream);
+
+/* YOLO PSA attention core (nn.py:111-122): per frame, per head:
+ *   out[c, i] = sum_j v[c, j] softmax_j(q[:, i] . k[:, j] * scale)
+ * qkv view [N, h, w, nh*(2*dk+dh)] (per head: q dk | k dk | v dh), out view [N,h,w,nh*dh].
+ * vout (optional, ptr may be NULL): v gathered head-major [N,h,w,nh*dh] — the
+ * ``v.reshape(b, c, h, w)`` operand of the depthwise positional conv (nn.py:122). */
+int prpe_psa_attention(const prpe_view* qkv, const prpe_view* out, const prpe_view* vout,
+                       int32_t nh, int32_t dk, int32_t dh, float scale, void* stream);
+
+/* YOLO Head eval decode (nn.py:255-270 + DFL nn.py:212-225 + make_anchors util.py:85-96).
+ * head: [B, A, 64+nc] rows (per anchor: 64 DFL logits, nc class logits), levels given by
+ * (h_l, w_l, stride_l) in anchor order; out: [B, 4+nc, A] = (cx,cy,w,h)*stride, sigmoid(cls). */
+int prpe_dfl_decode(const float* head, float* out, int32_t B, int32_t nc, int32_t nlevels,
+                    const int32_t* level_hw /* [nlevels*2] host */, const float* strides /* host */,
+                    void* stream);
+
+/* Row-wise L2 normalisation: norm = ||x||_2, emb = x / norm (net_adaface.py:334-337). */
+int prpe_l2norm(const float* x, float* emb, float* norm, int32_t rows, int32_t C, void* stream);
+
+/*
+ * yolopt.util.non_max_suppression (training/yolopt/util.py:123-169), batched, on device.
+ * pred: [B, 4+nc, N] when layout = 0; [B, N, 4+nc] when layout = 1 (same arithmetic as the
+ * reference on a transposed tensor). Candidates: max class score > conf; boxes cxcywh ->
+ * xyxy; nc==1: best class; nc>1: every (box, class) with score > conf; stable descending
+ * score order (ties by index), <= max_nms candidates, class offset 7680*cls,
+ * greedy suppression IoU > iou (torchvision.ops.nms), <= max_det kept.
+ * out: [B, max_det, 6] (x1,y1,x2,y2,conf,cls), count: [B] int32. No host sync.
+ * workspace: >= prpe_nms_workspace_bytes(B, N, nc, max_nms) bytes.
+ * The reference's wall-clock cut-off (util.py:133-134,166-167) is not reproduced.
+ */
+int64_t prpe_nms_workspace_bytes(int32_t B, int32_t N, int32_t nc, int32_t max_nms);
+int prpe_nms(const float* pred, int32_t B, int32_t N, int32_t nc, int32_t layout,
+             float conf, float iou, int32_t max_nms, int32_t max_det,
+             float* out, int32_t* count, void* workspace, int64_t workspace_bytes, void* stream);
+
+/*
+ * PoseEstimationModule._get_keypoints_from_heatmaps (pose_estimation/module.py:237-296):
+ * per (frame, keypoint) softmax over H*W, coords = (E[x]+0.5)/W, (E[y]+0.5)/H, score =
+ * max prob (* clamp(sqrt(box area)/96, .5, 2) when boxes != NULL, boxes [B,4] x1y1x2y2).
+ * heat: [B, K, H, W] contiguous. argmax (optional, may be NULL): [B,K] int32 flat index of
+ * the max (first occurrence) = the hard-argmax keypoint.
+ */
+int prpe_softargmax(const float* heat, int32_t B, int32_t K, int32_t H, int32_t W,
+                    const float* boxes, float* coords, float* scores, int32_t* argmax,
+                    void* stream);
+
+/* ABI version / build info. */
+int prpe_abi_version(void);
+const char* prpe_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRPE_H_ */

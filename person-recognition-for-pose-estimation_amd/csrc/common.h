@@ -1,0 +1,68 @@
+// Shared device helpers for the prpe HIP kernels (gfx950 / CDNA4, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+#include "prpe.h"
+
+#define PRPE_EINVAL (-22)
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline int launch_status() {
+  hipError_t e = hipGetLastError();
+  return e == hipSuccess ? 0 : static_cast<int>(e);
+}
+
+// Activation applied in every epilogue. Accurate libm forms (expf/erff), not fast-math,
+// so results track the fp32 CPU reference to a few ulp.
+__device__ __forceinline__ float apply_act(float v, int act, float slope) {
+  switch (act) {
+    case PRPE_ACT_RELU: return v > 0.f ? v : 0.f;
+    case PRPE_ACT_SILU: return v / (1.f + expf(-v));
+    case PRPE_ACT_PRELU: return v >= 0.f ? v : v * slope;
+    case PRPE_ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752440f));
+    case PRPE_ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    default: return v;
+  }
+}
+
+// fp32 -> (hi, lo) bf16 pair, hi = RNE(x), lo = RNE(x - hi). |x - hi - lo| <= 2^-17 |x|.
+__device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {
+  hi = (__bf16)x;
+  lo = (__bf16)(x - (float)hi);
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double warp_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Bijective XCD-aware block remap (MI355X: blocks b and b+8 share an XCD/L2).
+// Consecutive logical ids land on the same XCD, so tiles that share an operand panel
+// share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int nx = 8;
+  int xcd = bid % nx, q = nwg / nx, r = nwg % nx;
+  int start = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return start + bid / nx;
+}
+
+static inline bool view_ok(const prpe_view* v) {
+  return v && v->ptr && v->n > 0 && v->h > 0 && v->w > 0 && v->c > 0;
+}

@@ -1,0 +1,394 @@
+// Memory-bound kernels of the hot path (HBM / L2 bound, VALU, wave64).
+//   upconv3x3     : bilinear-upsample o conv3x3 rewrite, stage 2 (interp of per-tap GEMMs)
+//   dwconv        : depthwise kxk conv + folded BN + act (+ residual)
+//   maxpool       : kxk/s/p max pooling
+//   upsample2x    : nearest x2
+//   norm_sigmoid  : per-sample per-channel standardisation + sigmoid
+//   layernorm     : row LayerNorm (+ReLU)
+//   l2norm        : row L2 normalisation
+//   dfl_decode    : YOLO head eval decode (DFL softmax-expectation, anchors, strides, sigmoid)
+#include "common.h"
+
+namespace {
+
+__device__ __forceinline__ int64_t voff(const prpe_view& v, int n, int h, int w, int c) {
+  return (int64_t)n * v.sn + (int64_t)h * v.sh + (int64_t)w * v.sw + (int64_t)c * v.sc;
+}
+
+// PyTorch upsample_bilinear2d source index (aten/src/ATen/native/UpSample.h semantics):
+// align_corners: src = dst * (in-1)/(out-1); else src = max(0, (dst+0.5)*in/out - 0.5).
+__device__ __forceinline__ void bilin_src(int dst, int in, int out, int ac, int& i0, int& i1, float& l1) {
+  float src;
+  if (ac) {
+    const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+    src = scale * (float)dst;
+  } else {
+    const float scale = (float)in / (float)out;
+    src = scale * ((float)dst + 0.5f) - 0.5f;
+    src = src < 0.f ? 0.f : src;
+  }
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 < in - 1 ? i0 + 1 : i0;
+  l1 = src - (float)i0;
+}
+
+struct UpK {
+  prpe_view z, y;
+  int Co, ac;
+  const float* scale; const float* bias; const float* slope; int act;
+  int64_t total;  // N*Ho*Wo*(Co/VW)
+};
+
+// One thread = VW consecutive output channels of one output pixel.
+template <int VW>
+__global__ __launch_bounds__(256) void upconv3x3_kernel(UpK p) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.total) return;
+  const int cgroups = p.Co / VW;
+  const int cg = (int)(t % cgroups);
+  int64_t pix = t / cgroups;
+  const int Ho = p.y.h, Wo = p.y.w, Hi = p.z.h, Wi = p.z.w;
+  const int ox = (int)(pix % Wo); pix /= Wo;
+  const int oy = (int)(pix % Ho);
+  const int n = (int)(pix / Ho);
+  const int c0 = cg * VW;
+  float acc[VW];
+#pragma unroll
+  for (int v = 0; v < VW; ++v) acc[v] = 0.f;
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int yy = oy + dy - 1;
+    if ((unsigned)yy >= (unsigned)Ho) continue;
+    int y0, y1; float ly;
+    bilin_src(yy, Hi, Ho, p.ac, y0, y1, ly);
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int xx = ox + dx - 1;
+      if ((unsigned)xx >= (unsigned)Wo) continue;
+      int x0, x1; float lx;
+      bilin_src(xx, Wi, Wo, p.ac, x0, x1, lx);
+      const int tap = dy * 3 + dx;
+      const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx;
+      const float w10 = ly * (1.f - lx), w11 = ly * lx;
+      const float* z = p.z.ptr + (int64_t)n * p.z.sn + (int64_t)(tap * p.Co + c0) * p.z.sc;
+      const float* a = z + (int64_t)y0 * p.z.sh + (int64_t)x0 * p.z.sw;
+      const float* b = z + (int64_t)y0 * p.z.sh + (int64_t)x1 * p.z.sw;
+      const float* c = z + (int64_t)y1 * p.z.sh + (int64_t)x0 * p.z.sw;
+      const float* d = z + (int64_t)y1 * p.z.sh + (int64_t)x1 * p.z.sw;
+      if constexpr (VW == 4) {
+        const float4 A = *reinterpret_cast<const float4*>(a), B = *reinterpret_cast<const float4*>(b);
+        const float4 C = *reinterpret_cast<const float4*>(c), D = *reinterpret_cast<const float4*>(d);
+        acc[0] += w00 * A.x + w01 * B.x + w10 * C.x + w11 * D.x;
+        acc[1] += w00 * A.y + w01 * B.y + w10 * C.y + w11 * D.y;
+        acc[2] += w00 * A.z + w01 * B.z + w10 * C.z + w11 * D.z;
+        acc[3] += w00 * A.w + w01 * B.w + w10 * C.w + w11 * D.w;
+      } else {
+        acc[0] += w00 * a[0] + w01 * b[0] + w10 * c[0] + w11 * d[0];
+      }
+    }
+  }
+  float out[VW];
+#pragma unroll
+  for (int v = 0; v < VW; ++v) {
+    const int co = c0 + v;
+    const float s = p.scale ? p.scale[co] : 1.f;
+    const float bb = p.bias ? p.bias[co] : 0.f;
+    out[v] = apply_act(acc[v] * s + bb, p.act, p.slope ? p.slope[co] : 0.f);
+  }
+  float* y = p.y.ptr + voff(p.y, n, oy, ox, c0);
+  if constexpr (VW == 4) {
+    if (p.y.sc == 1) {
+      *reinterpret_cast<float4*>(y) = make_float4(out[0], out[1], out[2], out[3]);
+      return;
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < VW; ++v) y[(int64_t)v * p.y.sc] = out[v];
+}
+
+// ------------------------------------------------------------------------- dwconv
+struct DwK {
+  prpe_view x, y, r;
+  const float* w; int k, stride, pad;
+  const float* scale; const float* bias; int act;
+  int64_t total;
+};
+__global__ __launch_bounds__(256) void dwconv_kernel(DwK p) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.total) return;
+  const int C = p.y.c;
+  const int c = (int)(t % C);
+  int64_t q = t / C;
+  const int ow = (int)(q % p.y.w); q /= p.y.w;
+  const int oh = (int)(q % p.y.h);
+  const int n = (int)(q / p.y.h);
+  float acc = 0.f;
+  const float* wc = p.w + (int64_t)c * p.k * p.k;
+  for (int kh = 0; kh < p.k; ++kh) {
+    const int ih = oh * p.stride - p.pad + kh;
+    if ((unsigned)ih >= (unsigned)p.x.h) continue;
+    for (int kw = 0; kw < p.k; ++kw) {
+      const int iw = ow * p.stride - p.pad + kw;
+      if ((unsigned)iw >= (unsigned)p.x.w) continue;
+      acc += p.x.ptr[voff(p.x, n, ih, iw, c)] * wc[kh * p.k + kw];
+    }
+  }
+  float v = acc * (p.scale ? p.scale[c] : 1.f) + (p.bias ? p.bias[c] : 0.f);
+  v = apply_act(v, p.act, 0.f);
+  if (p.r.ptr) v += p.r.ptr[voff(p.r, n, oh, ow, c)];
+  p.y.ptr[voff(p.y, n, oh, ow, c)] = v;
+}
+
+// ------------------------------------------------------------------------- maxpool
+struct PoolK { prpe_view x, y; int k, stride, pad; int64_t total; };
+__global__ __launch_bounds__(256) void maxpool_kernel(PoolK p) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.total) return;
+  const int C = p.y.c;
+  const int c = (int)(t % C);
+  int64_t q = t / C;
+  const int ow = (int)(q % p.y.w); q /= p.y.w;
+  const int oh = (int)(q % p.y.h);
+  const int n = (int)(q / p.y.h);
+  float m = -INFINITY;
+  for (int kh = 0; kh < p.k; ++kh) {
+    const int ih = oh * p.stride - p.pad + kh;
+    if ((unsigned)ih >= (unsigned)p.x.h) continue;
+    for (int kw = 0; kw < p.k; ++kw) {
+      const int iw = ow * p.stride - p.pad + kw;
+      if ((unsigned)iw >= (unsigned)p.x.w) continue;
+      const float v = p.x.ptr[voff(p.x, n, ih, iw, c)];
+      m = (v > m || v != v) ? v : m;   // NaN propagates like torch max_pool2d
+    }
+  }
+  p.y.ptr[voff(p.y, n, oh, ow, c)] = m;
+}
+
+struct Up2K { prpe_view x, y; int64_t total; };
+__global__ __launch_bounds__(256) void upsample2x_kernel(Up2K p) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.total) return;
+  const int C = p.y.c;
+  const int c = (int)(t % C);
+  int64_t q = t / C;
+  const int ow = (int)(q % p.y.w); q /= p.y.w;
+  const int oh = (int)(q % p.y.h);
+  const int n = (int)(q / p.y.h);
+  p.y.ptr[voff(p.y, n, oh, ow, c)] = p.x.ptr[voff(p.x, n, oh >> 1, ow >> 1, c)];
+}
+
+// ------------------------------------------------------------------------- norm_sigmoid
+// one workgroup per sample; channels <= 4; double accumulation (two passes)
+__global__ __launch_bounds__(256) void norm_sigmoid_kernel(prpe_view x, prpe_view y) {
+  const int n = blockIdx.x;
+  const int C = x.c, HW = x.h * x.w;
+  __shared__ double red[4][4];
+  __shared__ float stat[4][2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int c = 0; c < C; ++c) {
+    double s = 0.0;
+    for (int i = threadIdx.x; i < HW; i += blockDim.x) s += x.ptr[voff(x, n, i / x.w, i % x.w, c)];
+    s = warp_sum_d(s);
+    if (lane == 0) red[wave][0] = s;
+    __syncthreads();
+    const float mean = (float)((red[0][0] + red[1][0] + red[2][0] + red[3][0]) / HW);
+    __syncthreads();
+    // std of the centred values (modify_models.py:84-85): unbiased, around their own mean
+    double s1 = 0.0, s2 = 0.0;
+    for (int i = threadIdx.x; i < HW; i += blockDim.x) {
+      const double d = (double)(x.ptr[voff(x, n, i / x.w, i % x.w, c)] - mean);
+      s1 += d; s2 += d * d;
+    }
+    s1 = warp_sum_d(s1); s2 = warp_sum_d(s2);
+    if (lane == 0) { red[wave][1] = s1; red[wave][2] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const double S1 = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+      const double S2 = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+      const double var = (S2 - S1 * S1 / HW) / (HW - 1);
+      stat[c][0] = mean;
+      stat[c][1] = (float)sqrt(var > 0.0 ? var : 0.0);
+    }
+    __syncthreads();
+  }
+  for (int i = threadIdx.x; i < HW * C; i += blockDim.x) {
+    const int c = i % C, pix = i / C;
+    const int h = pix / x.w, w = pix % x.w;
+    const float v = (x.ptr[voff(x, n, h, w, c)] - stat[c][0]) / (stat[c][1] + 1e-6f);
+    y.ptr[voff(y, n, h, w, c)] = 1.f / (1.f + expf(-v));
+  }
+}
+
+// ------------------------------------------------------------------------- layernorm
+// one wave per row
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int64_t xs, float* y, int64_t ys,
+                                                        int64_t rows, int C, const float* g, const float* b,
+                                                        float eps, int relu) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const float* xr = x + row * xs;
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += xr[c];
+  const float mean = warp_sum(s) / (float)C;
+  float v = 0.f;
+  for (int c = lane; c < C; c += 64) { const float d = xr[c] - mean; v += d * d; }
+  const float var = warp_sum(v) / (float)C;
+  const float rstd = 1.f / sqrtf(var + eps);
+  float* yr = y + row * ys;
+  for (int c = lane; c < C; c += 64) {
+    float o = (xr[c] - mean) * rstd * g[c] + b[c];
+    if (relu) o = o > 0.f ? o : 0.f;
+    yr[c] = o;
+  }
+}
+
+// ------------------------------------------------------------------------- l2norm
+__global__ __launch_bounds__(256) void l2norm_kernel(const float* x, float* emb, float* norm, int rows, int C) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const float* xr = x + (int64_t)row * C;
+  double s = 0.0;
+  for (int c = lane; c < C; c += 64) s += (double)xr[c] * xr[c];
+  const float nrm = (float)sqrt(warp_sum_d(s));
+  for (int c = lane; c < C; c += 64) emb[(int64_t)row * C + c] = xr[c] / nrm;
+  if (lane == 0) norm[row] = nrm;
+}
+
+// ------------------------------------------------------------------------- dfl decode
+struct DflK {
+  const float* head; float* out; int B, nc, A, nlev;
+  int hw[8][2]; float stride[4]; int off[5];
+};
+__global__ __launch_bounds__(256) void dfl_decode_kernel(DflK p) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= p.B * p.A) return;
+  const int b = t / p.A, a = t % p.A;
+  int l = 0;
+  while (l + 1 < p.nlev && a >= p.off[l + 1]) ++l;
+  const int ia = a - p.off[l];
+  const int w = p.hw[l][1];
+  const float ax = (float)(ia % w) + 0.5f, ay = (float)(ia / w) + 0.5f;
+  const float st = p.stride[l];
+  const int no = 64 + p.nc;
+  const float* h = p.head + ((int64_t)b * p.A + a) * no;
+  float d[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    float m = -INFINITY;
+    for (int i = 0; i < 16; ++i) m = fmaxf(m, h[s * 16 + i]);
+    float e[16], sum = 0.f;
+    for (int i = 0; i < 16; ++i) { e[i] = expf(h[s * 16 + i] - m); sum += e[i]; }
+    float acc = 0.f;
+    for (int i = 0; i < 16; ++i) acc += (e[i] / sum) * (float)i;
+    d[s] = acc;
+  }
+  const float x1 = ax - d[0], y1 = ay - d[1], x2 = ax + d[2], y2 = ay + d[3];
+  float* o = p.out + (int64_t)b * (4 + p.nc) * p.A + a;
+  o[0] = ((x1 + x2) / 2.f) * st;
+  o[(int64_t)p.A] = ((y1 + y2) / 2.f) * st;
+  o[(int64_t)2 * p.A] = (x2 - x1) * st;
+  o[(int64_t)3 * p.A] = (y2 - y1) * st;
+  for (int c = 0; c < p.nc; ++c) o[(int64_t)(4 + c) * p.A] = 1.f / (1.f + expf(-h[64 + c]));
+}
+
+inline unsigned nblocks(int64_t total, int bs = 256) { return (unsigned)((total + bs - 1) / bs); }
+
+}  // namespace
+
+extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,
+                              const float* scale, const float* bias, const float* slope, int32_t act,
+                              void* stream) {
+  if (!view_ok(z) || !view_ok(y) || z->n != y->n || z->c != 9 * y->c) return PRPE_EINVAL;
+  if (act == PRPE_ACT_PRELU && !slope) return PRPE_EINVAL;
+  UpK p{};
+  p.z = *z; p.y = *y; p.Co = y->c; p.ac = align_corners ? 1 : 0;
+  p.scale = scale; p.bias = bias; p.slope = slope; p.act = act;
+  const bool v4 = (y->c % 4 == 0) && z->sc == 1 && (z->sw % 4 == 0) && (z->sh % 4 == 0) &&
+                  (z->sn % 4 == 0) && ((uintptr_t)z->ptr % 16 == 0) &&
+                  (y->sc != 1 || ((y->sw % 4 == 0) && (y->sh % 4 == 0) && (y->sn % 4 == 0) &&
+                                  ((uintptr_t)y->ptr % 16 == 0)));
+  const int64_t pix = (int64_t)y->n * y->h * y->w;
+  hipStream_t st = as_stream(stream);
+  if (v4) {
+    p.total = pix * (y->c / 4);
+    hipLaunchKernelGGL(upconv3x3_kernel<4>, dim3(nblocks(p.total)), dim3(256), 0, st, p);
+  } else {
+    p.total = pix * y->c;
+    hipLaunchKernelGGL(upconv3x3_kernel<1>, dim3(nblocks(p.total)), dim3(256), 0, st, p);
+  }
+  return launch_status();
+}
+
+extern "C" int prpe_dwconv(const prpe_view* x, const prpe_view* y, const prpe_view* res, const float* w,
+                           int32_t k, int32_t stride, int32_t pad, const float* scale, const float* bias,
+                           int32_t act, void* stream) {
+  if (!view_ok(x) || !view_ok(y) || !w || x->c != y->c || x->n != y->n || k <= 0 || stride <= 0) return PRPE_EINVAL;
+  if ((x->h + 2 * pad - k) / stride + 1 != y->h || (x->w + 2 * pad - k) / stride + 1 != y->w) return PRPE_EINVAL;
+  if (act == PRPE_ACT_PRELU) return PRPE_EINVAL;
+  DwK p{};
+  p.x = *x; p.y = *y;
+  if (res && res->ptr) p.r = *res;
+  p.w = w; p.k = k; p.stride = stride; p.pad = pad; p.scale = scale; p.bias = bias; p.act = act;
+  p.total = (int64_t)y->n * y->h * y->w * y->c;
+  hipLaunchKernelGGL(dwconv_kernel, dim3(nblocks(p.total)), dim3(256), 0, as_stream(stream), p);
+  return launch_status();
+}
+
+extern "C" int prpe_maxpool(const prpe_view* x, const prpe_view* y, int32_t k, int32_t stride, int32_t pad,
+                            void* stream) {
+  if (!view_ok(x) || !view_ok(y) || x->c != y->c || x->n != y->n || k <= 0 || stride <= 0) return PRPE_EINVAL;
+  if ((x->h + 2 * pad - k) / stride + 1 != y->h || (x->w + 2 * pad - k) / stride + 1 != y->w) return PRPE_EINVAL;
+  PoolK p{*x, *y, k, stride, pad, (int64_t)y->n * y->h * y->w * y->c};
+  hipLaunchKernelGGL(maxpool_kernel, dim3(nblocks(p.total)), dim3(256), 0, as_stream(stream), p);
+  return launch_status();
+}
+
+extern "C" int prpe_upsample_nearest2x(const prpe_view* x, const prpe_view* y, void* stream) {
+  if (!view_ok(x) || !view_ok(y) || x->c != y->c || x->n != y->n || y->h != 2 * x->h || y->w != 2 * x->w)
+    return PRPE_EINVAL;
+  Up2K p{*x, *y, (int64_t)y->n * y->h * y->w * y->c};
+  hipLaunchKernelGGL(upsample2x_kernel, dim3(nblocks(p.total)), dim3(256), 0, as_stream(stream), p);
+  return launch_status();
+}
+
+extern "C" int prpe_norm_sigmoid(const prpe_view* x, const prpe_view* y, void* stream) {
+  if (!view_ok(x) || !view_ok(y) || x->c > 4 || x->c != y->c || x->n != y->n || x->h != y->h || x->w != y->w ||
+      x->h * x->w < 2)
+    return PRPE_EINVAL;
+  hipLaunchKernelGGL(norm_sigmoid_kernel, dim3(x->n), dim3(256), 0, as_stream(stream), *x, *y);
+  return launch_status();
+}
+
+extern "C" int prpe_layernorm(const float* x, int64_t xs, float* y, int64_t ys, int64_t rows, int32_t C,
+                              const float* g, const float* b, float eps, int32_t relu, void* stream) {
+  if (!x || !y || !g || !b || rows <= 0 || C <= 0) return PRPE_EINVAL;
+  hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, as_stream(stream), x, xs, y,
+                     ys, rows, C, g, b, eps, relu);
+  return launch_status();
+}
+
+extern "C" int prpe_l2norm(const float* x, float* emb, float* norm, int32_t rows, int32_t C, void* stream) {
+  if (!x || !emb || !norm || rows <= 0 || C <= 0) return PRPE_EINVAL;
+  hipLaunchKernelGGL(l2norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), x, emb, norm, rows, C);
+  return launch_status();
+}
+
+extern "C" int prpe_dfl_decode(const float* head, float* out, int32_t B, int32_t nc, int32_t nlev,
+                               const int32_t* level_hw, const float* strides, void* stream) {
+  if (!head || !out || B <= 0 || nc <= 0 || nlev <= 0 || nlev > 4 || !level_hw || !strides) return PRPE_EINVAL;
+  DflK p{};
+  p.head = head; p.out = out; p.B = B; p.nc = nc; p.nlev = nlev;
+  int a = 0;
+  for (int l = 0; l < nlev; ++l) {
+    p.hw[l][0] = level_hw[2 * l]; p.hw[l][1] = level_hw[2 * l + 1];
+    p.stride[l] = strides[l]; p.off[l] = a;
+    a += level_hw[2 * l] * level_hw[2 * l + 1];
+  }
+  p.off[nlev] = a;
+  p.A = a;
+  hipLaunchKernelGGL(dfl_decode_kernel, dim3(nblocks((int64_t)B * a)), dim3(256), 0, as_stream(stream), p);
+  return launch_status();
+}

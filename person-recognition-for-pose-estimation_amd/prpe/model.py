@@ -1,0 +1,131 @@
+"""Drop-in for the reference ``CombinedModel`` (training/modify_models.py:462-494) on MI355X.
+
+Same surface the eval steps touch:
+  * ``set_task(name)`` with the reference's supported list and ValueError message;
+  * ``model(images)`` routes the trunk features to one branch and returns the reference's
+    per-task types: detection -> Tensor [B, 4+1, 525]; pose -> object with ``.heatmaps``
+    [B,17,64,48]; face_recognition -> (embeddings [B,512], norms [B,1]);
+  * ``state_dict()/load_state_dict()`` with the reference's 2130 keys;
+  * ``model.yolo_face.yolo.head.stride`` / ``yolo_person...`` (a fresh ``Head`` after
+    ``modify_yolo`` has stride zeros, nn.py:238 -> eval boxes are 0; honoured as given);
+  * ``model.ada_face.head.kernel`` for the face-recognition eval logits.
+Plus ``forward_all(x)``: trunk once, then face-YOLO + AdaFace + ViTPose (BASELINE config 4).
+
+Eval-only: the reference's training outputs/backward are out of scope.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from types import SimpleNamespace
+
+import torch
+
+from . import arch
+from .engine import Engine
+
+
+@dataclass
+class PoseOutput:
+    """Stands in for transformers' VitPoseEstimatorOutput (the callers read ``.heatmaps``)."""
+    heatmaps: torch.Tensor
+    loss: torch.Tensor | None = None
+
+
+class CombinedModel:
+    SUPPORTED_TASKS = ["face_detection", "person_detection", "pose_estimation", "face_recognition"]
+
+    def __init__(self, state_dict: dict | None = None, device="cuda", precision="auto"):
+        self.current_task = "person_detection"
+        self.device = torch.device(device)
+        self.training = False
+        self.precision = precision
+        self._sd = {}
+        self.yolo_face = SimpleNamespace(yolo=SimpleNamespace(head=SimpleNamespace(stride=torch.zeros(3))))
+        self.yolo_person = SimpleNamespace(yolo=SimpleNamespace(head=SimpleNamespace(stride=torch.zeros(3))))
+        self.ada_face = SimpleNamespace(head=SimpleNamespace(kernel=None))
+        self.engine = None
+        if state_dict is not None:
+            self.load_state_dict(state_dict)
+
+    # ------------------------------------------------------------------ nn.Module-like API
+    def load_state_dict(self, state_dict, strict: bool = True):
+        keys = {k for k, _, _ in arch.state_dict_spec()}
+        missing = [k for k in keys if k not in state_dict and k != "ada_face.head.kernel"]
+        unexpected = [k for k in state_dict if k not in keys]
+        if strict and (missing or unexpected):
+            raise KeyError(f"state_dict mismatch: missing={missing[:5]} unexpected={unexpected[:5]}")
+        self._sd = {k: v.detach().cpu() for k, v in state_dict.items()}
+        if "ada_face.head.kernel" in self._sd:
+            self.ada_face.head.kernel = self._sd["ada_face.head.kernel"].to(self.device)
+        self.engine = Engine(self._sd, self.device, self.precision)
+        return SimpleNamespace(missing_keys=missing, unexpected_keys=unexpected)
+
+    def state_dict(self):
+        return dict(self._sd)
+
+    def to(self, device):
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise RuntimeError("prpe runs on MI355X (HIP) only; no CPU path")
+        if device != self.device:
+            self.device = device
+            if self._sd:
+                self.load_state_dict(self._sd, strict=False)
+        return self
+
+    def float(self):
+        return self
+
+    def eval(self):
+        self.training = False
+        return self
+
+    def train(self, mode: bool = True):
+        if mode:
+            raise NotImplementedError("training-mode outputs/backward are out of scope (eval hot path only)")
+        return self.eval()
+
+    def set_task(self, task_name):
+        if task_name not in self.SUPPORTED_TASKS:
+            raise ValueError(f"Task {task_name} not supported. Available tasks: {', '.join(self.SUPPORTED_TASKS)}")
+        self.current_task = task_name
+
+    # ------------------------------------------------------------------ forward
+    def _check_input(self, x):
+        if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+                and x.shape[1] == 3):
+            raise ValueError("expected float32 CUDA(HIP) frames [B,3,H,W]")
+        return x
+
+    @torch.no_grad()
+    def forward(self, x):
+        x = self._check_input(x)
+        e = self.engine
+        feat = e.trunk(x)
+        t = self.current_task
+        if t == "pose_estimation":
+            return PoseOutput(heatmaps=e.vitpose(feat))
+        if t == "person_detection":
+            return e.yolo("yolo_person", feat, self._stride(self.yolo_person))
+        if t == "face_detection":
+            return e.yolo("yolo_face", feat, self._stride(self.yolo_face))
+        return e.adaface(feat)
+
+    __call__ = forward
+
+    @torch.no_grad()
+    def forward_all(self, x, face_stride=None):
+        """Trunk once -> face-YOLO det, AdaFace (emb, norm), ViTPose heatmaps."""
+        x = self._check_input(x)
+        e = self.engine
+        feat = e.trunk(x)
+        stride = face_stride if face_stride is not None else self._stride(self.yolo_face)
+        det = e.yolo("yolo_face", feat, stride)
+        emb, norm = e.adaface(feat)
+        heat = e.vitpose(feat)
+        return {"det": det, "emb": emb, "norm": norm, "heatmaps": heat}
+
+    @staticmethod
+    def _stride(branch):
+        s = branch.yolo.head.stride
+        return [float(v) for v in (s.tolist() if isinstance(s, torch.Tensor) else s)]

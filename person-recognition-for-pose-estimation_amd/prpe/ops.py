@@ -1,0 +1,143 @@
+"""Torch-tensor level wrappers over the C ABI (device buffers come from PyTorch-ROCm).
+
+Tensors are float32 on the GPU with a *logical NHWC* shape [N, H, W, C] and arbitrary
+strides (channel slices of concat buffers, NCHW inputs via ``permute``, broadcast
+residuals with stride 0 ...). Every call launches on the current torch stream.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from ._lib import ACT, RES_NONE, ConvDesc, View, check, lib
+
+
+def _stream() -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def view(t: torch.Tensor | None) -> View:
+    """prpe_view of a 4-D logical-NHWC tensor (or a null view for None)."""
+    if t is None:
+        return View()
+    assert t.dim() == 4 and t.dtype == torch.float32 and t.is_cuda, (t.shape, t.dtype, t.device)
+    n, h, w, c = t.shape
+    sn, sh, sw, sc = t.stride()
+    return View(t.data_ptr(), n, h, w, c, sn, sh, sw, sc)
+
+
+def nhwc(t: torch.Tensor) -> torch.Tensor:
+    """Logical NHWC view of an NCHW tensor (no copy)."""
+    return t.permute(0, 2, 3, 1)
+
+
+def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, tile=0):
+    """y = EPI(conv(PRO(x))) with a ``ConvPack`` (see prpe.pack)."""
+    d = ConvDesc()
+    d.x = view(x)
+    d.y = view(y)
+    d.res = view(res)
+    d.kh, d.kw, d.stride, d.pad = pack.kh, pack.kw, pack.stride, pack.pad
+    d.w_hi, d.w_lo, d.w_lo2 = pack.w_hi.data_ptr(), pack.w_lo.data_ptr(), pack.w_lo2.data_ptr()
+    d.k_pad, d.co_pad = pack.k_pad, pack.co_pad
+    d.scale, d.bias, d.slope = _ptr(pack.scale), _ptr(pack.bias), _ptr(pack.slope)
+    d.in_scale, d.in_bias = _ptr(pack.in_scale), _ptr(pack.in_bias)
+    d.act = ACT[act if act is not None else pack.act]
+    d.res_mode = res_mode
+    d.precision = precision
+    d.tile = tile
+    check(lib().prpe_conv2d(C.byref(d), _stream()), f"prpe_conv2d[{pack.name}]")
+    return y
+
+
+def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none"):
+    check(lib().prpe_upconv3x3(C.byref(view(z)), C.byref(view(y)), 1 if align_corners else 0,
+                               _ptr(scale), _ptr(bias), _ptr(slope), ACT[act], _stream()), "prpe_upconv3x3")
+    return y
+
+
+def dwconv(x, y, w, k, stride, pad, scale, bias, act="none", res=None):
+    check(lib().prpe_dwconv(C.byref(view(x)), C.byref(view(y)), C.byref(view(res)), w.data_ptr(), k, stride, pad,
+                            _ptr(scale), _ptr(bias), ACT[act], _stream()), "prpe_dwconv")
+    return y
+
+
+def maxpool(x, y, k, stride, pad):
+    check(lib().prpe_maxpool(C.byref(view(x)), C.byref(view(y)), k, stride, pad, _stream()), "prpe_maxpool")
+    return y
+
+
+def upsample_nearest2x(x, y):
+    check(lib().prpe_upsample_nearest2x(C.byref(view(x)), C.byref(view(y)), _stream()), "prpe_upsample_nearest2x")
+    return y
+
+
+def norm_sigmoid(x, y):
+    check(lib().prpe_norm_sigmoid(C.byref(view(x)), C.byref(view(y)), _stream()), "prpe_norm_sigmoid")
+    return y
+
+
+def layernorm(x2d, y2d, gamma, beta, eps=1e-12, relu=False):
+    rows, c = x2d.shape
+    check(lib().prpe_layernorm(x2d.data_ptr(), x2d.stride(0), y2d.data_ptr(), y2d.stride(0), rows, c,
+                               gamma.data_ptr(), beta.data_ptr(), eps, 1 if relu else 0, _stream()),
+          "prpe_layernorm")
+    return y2d
+
+
+def attention(qkv, out, B, L, H, D, scale):
+    check(lib().prpe_attention(qkv.data_ptr(), out.data_ptr(), B, L, H, D, scale, _stream()), "prpe_attention")
+    return out
+
+
+def psa_attention(qkv, out, vout, nh, dk, dh, scale):
+    check(lib().prpe_psa_attention(C.byref(view(qkv)), C.byref(view(out)), C.byref(view(vout)), nh, dk, dh, scale,
+                                   _stream()), "prpe_psa_attention")
+    return out
+
+
+def dfl_decode(head, out, nc, level_hw, strides):
+    B = head.shape[0]
+    hw = (C.c_int32 * (2 * len(level_hw)))(*[v for hw_ in level_hw for v in hw_])
+    st = (C.c_float * len(strides))(*[float(s) for s in strides])
+    check(lib().prpe_dfl_decode(head.data_ptr(), out.data_ptr(), B, nc, len(level_hw), hw, st, _stream()),
+          "prpe_dfl_decode")
+    return out
+
+
+def l2norm(x, emb, norm):
+    rows, c = x.shape
+    check(lib().prpe_l2norm(x.data_ptr(), emb.data_ptr(), norm.data_ptr(), rows, c, _stream()), "prpe_l2norm")
+    return emb, norm
+
+
+def nms(pred, layout, conf=0.001, iou=0.65, max_nms=30000, max_det=300):
+    """Batched device NMS -> (out [B,max_det,6], count [B] int32). layout 0: [B,4+nc,N]; 1: [B,N,4+nc]."""
+    pred = pred.contiguous()
+    B = pred.shape[0]
+    if layout == 0:
+        nc, N = pred.shape[1] - 4, pred.shape[2]
+    else:
+        N, nc = pred.shape[1], pred.shape[2] - 4
+    out = torch.empty(B, max_det, 6, device=pred.device, dtype=torch.float32)
+    cnt = torch.empty(B, device=pred.device, dtype=torch.int32)
+    check(lib().prpe_nms(pred.data_ptr(), B, N, nc, layout, conf, iou, max_nms, max_det, out.data_ptr(),
+                         cnt.data_ptr(), None, 0, _stream()), "prpe_nms")
+    return out, cnt
+
+
+def softargmax(heat, boxes=None, want_argmax=False):
+    heat = heat.contiguous()
+    B, K, H, W = heat.shape
+    coords = torch.empty(B, K, 2, device=heat.device, dtype=torch.float32)
+    scores = torch.empty(B, K, device=heat.device, dtype=torch.float32)
+    am = torch.empty(B, K, device=heat.device, dtype=torch.int32) if want_argmax else None
+    bx = boxes.contiguous().float() if boxes is not None else None
+    check(lib().prpe_softargmax(heat.data_ptr(), B, K, H, W, _ptr(bx), coords.data_ptr(), scores.data_ptr(),
+                                _ptr(am), _stream()), "prpe_softargmax")
+    return (coords, scores, am) if want_argmax else (coords, scores)

@@ -1,0 +1,104 @@
+"""Weight packing: reference state_dict tensors -> device-resident conv packs.
+
+A ``ConvPack`` holds the weight of one conv / linear in the layout the implicit-GEMM
+kernel streams (include/prpe.h, prpe_conv2d):
+  * W[co, ci, kh, kw] -> [co][(kh*KW + kw)*Ci + ci], zero-padded to [co_pad][k_pad]
+    (k_pad % 32 == 0, co_pad % 128 == 0), split into three bf16 planes
+    (p0 = RNE(w), p1 = RNE(w - p0), p2 = RNE(w - p0 - p1); p0+p1+p2 == w exactly);
+  * the epilogue's per-channel affine: eval BatchNorm folded exactly as PyTorch's CPU
+    batch_norm inference does (alpha = gamma / sqrt(var + eps), beta' = beta - mean*alpha),
+    with the conv bias folded in (bias*alpha + beta');
+  * optional PReLU slopes and an input-side (prologue) affine for pre-activation BN.
+Packing runs once at load time (host + one upload); nothing here is on the per-frame path.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+
+def _rup(v: int, m: int) -> int:
+    return (v + m - 1) // m * m
+
+
+@dataclass
+class ConvPack:
+    name: str
+    w_hi: torch.Tensor
+    w_lo: torch.Tensor
+    w_lo2: torch.Tensor
+    kh: int
+    kw: int
+    stride: int
+    pad: int
+    ci: int
+    co: int
+    k_pad: int
+    co_pad: int
+    scale: torch.Tensor | None = None
+    bias: torch.Tensor | None = None
+    slope: torch.Tensor | None = None
+    in_scale: torch.Tensor | None = None
+    in_bias: torch.Tensor | None = None
+    act: str = "none"
+
+    @property
+    def flops_per_pixel(self) -> int:
+        return 2 * self.co * self.ci * self.kh * self.kw
+
+
+def split_bf16(w: torch.Tensor, planes: int = 3):
+    """fp32 -> ``planes`` bf16 tensors (RNE splits); 3 planes reproduce fp32 exactly."""
+    r = w.float()
+    out = []
+    for _ in range(planes):
+        t = r.to(torch.bfloat16)
+        out.append(t)
+        r = r - t.float()
+    return out
+
+
+def bn_affine(sd, prefix, eps, conv_bias=None):
+    """(scale, shift) of an eval BatchNorm (+ preceding conv bias), fp32."""
+    var = sd[prefix + ".running_var"].float()
+    mean = sd[prefix + ".running_mean"].float()
+    g = sd.get(prefix + ".weight")
+    b = sd.get(prefix + ".bias")
+    g = torch.ones_like(var) if g is None else g.float()
+    b = torch.zeros_like(var) if b is None else b.float()
+    alpha = g / torch.sqrt(var + eps)
+    shift = b - mean * alpha
+    if conv_bias is not None:
+        shift = shift + conv_bias.float() * alpha
+    return alpha.contiguous(), shift.contiguous()
+
+
+def pack_matrix(name, w2d: torch.Tensor, kh, kw, ci, stride, pad, device, scale=None, bias=None,
+                slope=None, in_scale=None, in_bias=None, act="none") -> ConvPack:
+    """w2d: [co, K] with K ordered (kh, kw, ci)."""
+    co, K = w2d.shape
+    k_pad, co_pad = _rup(K, 32), _rup(co, 128)
+    wp = torch.zeros(co_pad, k_pad, dtype=torch.float32)
+    wp[:co, :K] = w2d.float()
+    p0, p1, p2 = split_bf16(wp, 3)
+    dev = lambda t: None if t is None else t.float().contiguous().to(device)
+    return ConvPack(name, p0.contiguous().to(device), p1.contiguous().to(device), p2.contiguous().to(device), kh, kw,
+                    stride, pad, ci, co, k_pad, co_pad, dev(scale), dev(bias), dev(slope), dev(in_scale),
+                    dev(in_bias), act)
+
+
+def pack_conv(name, w: torch.Tensor, stride=1, pad=0, device="cuda", **kw) -> ConvPack:
+    """w: [co, ci, kh, kw] (PyTorch layout)."""
+    co, ci, kh, kw_ = w.shape
+    w2d = w.float().permute(0, 2, 3, 1).reshape(co, kh * kw_ * ci)
+    return pack_matrix(name, w2d, kh, kw_, ci, stride, pad, device, **kw)
+
+
+def pack_upconv_taps(name, w: torch.Tensor, device="cuda") -> ConvPack:
+    """3x3 conv weight [co, ci, 3, 3] -> 1x1 pack with 9*co outputs (channel = tap*co + co'):
+    stage 1 of the exact upsample/conv rewrite (prpe_upconv3x3)."""
+    co, ci, kh, kw_ = w.shape
+    assert kh == 3 and kw_ == 3
+    w2d = w.float().permute(2, 3, 0, 1).reshape(9 * co, ci)   # [(tap, co), ci]
+    return pack_matrix(name, w2d, 1, 1, ci, 1, 0, device)

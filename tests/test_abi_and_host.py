@@ -1,0 +1,104 @@
+"""CPU: the C ABI library (loads, exports every symbol declared in include/prpe.h, rejects
+bad arguments without launching) and the host-side logic (weight packing, BN folding,
+state_dict layout, task routing API)."""
+import ctypes as C
+import os
+import re
+
+import pytest
+import torch
+
+from conftest import ROOT
+
+from prpe import _lib, arch, pack, synth
+from prpe.model import CombinedModel
+
+
+def _declared_symbols():
+    src = open(os.path.join(ROOT, "include", "prpe.h")).read()
+    return sorted(set(re.findall(r"\b(prpe_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _lib.lib()
+    decl = _declared_symbols()
+    assert len(decl) >= 15
+    for name in decl:
+        assert hasattr(L, name), name
+    assert set(decl) == set(_lib.SIGNATURES), "ctypes table must bind exactly the header's entry points"
+    assert L.prpe_abi_version() == _lib.ABI_VERSION
+    assert b"gfx950" in L.prpe_build_info()
+
+
+def test_invalid_arguments_are_rejected_before_launch():
+    L = _lib.lib()
+    d = _lib.ConvDesc()               # null views
+    assert L.prpe_conv2d(C.byref(d), None) == -22
+    assert L.prpe_nms(None, 1, 1, 1, 0, 0.001, 0.65, 30000, 300, None, None, None, 0, None) == -22
+    assert L.prpe_softargmax(None, 1, 1, 1, 1, None, None, None, None, None) == -22
+    assert L.prpe_attention(None, None, 1, 192, 12, 64, 0.125, None) == -22
+    bad = _lib.View(0x1000, 1, 4, 4, 8, 128, 32, 8, 1)
+    assert L.prpe_norm_sigmoid(C.byref(bad), C.byref(bad), None) == -22    # > 4 channels
+
+
+def test_state_dict_spec_is_complete():
+    spec = arch.state_dict_spec()
+    assert len(spec) == 2130
+    n = sum(int(torch.tensor(s).prod()) if len(s) else 1 for _, s, _ in spec)
+    assert n == 215109568   # numel of the reference CombinedModel.state_dict()
+
+
+def test_pack_layout_and_split():
+    w = torch.randn(5, 3, 3, 3)
+    p = pack.pack_conv("t", w, 1, 1, "cpu")
+    assert p.k_pad == 32 and p.co_pad == 128 and (p.kh, p.kw, p.ci, p.co) == (3, 3, 3, 5)
+    full = p.w_hi.float() + p.w_lo.float()
+    # k = (kh*3 + kw)*Ci + ci
+    for co in range(5):
+        for kh in range(3):
+            for kw in range(3):
+                for ci in range(3):
+                    k = (kh * 3 + kw) * 3 + ci
+                    assert abs(full[co, k] - w[co, ci, kh, kw]) <= 2 ** -16 * abs(w[co, ci, kh, kw]) + 1e-30
+    assert torch.all(full[5:] == 0) and torch.all(full[:, 27:] == 0)
+
+
+def test_upconv_tap_pack_order():
+    w = torch.randn(4, 6, 3, 3)
+    p = pack.pack_upconv_taps("t", w, "cpu")
+    full = p.w_hi.float() + p.w_lo.float()
+    for tap in range(9):
+        for co in range(4):
+            ref = w[co, :, tap // 3, tap % 3]
+            torch.testing.assert_close(full[tap * 4 + co, :6], ref, rtol=2 ** -15, atol=1e-7)
+
+
+def test_bn_fold_matches_torch_eval_batchnorm():
+    sd = {"b.weight": torch.rand(7) + 0.5, "b.bias": torch.randn(7), "b.running_mean": torch.randn(7),
+          "b.running_var": torch.rand(7) + 0.1}
+    s, t = pack.bn_affine(sd, "b", 1e-3, conv_bias=torch.ones(7))
+    x = torch.randn(2, 7, 3, 3)
+    ref = torch.nn.functional.batch_norm(x + 1.0, sd["b.running_mean"], sd["b.running_var"], sd["b.weight"],
+                                         sd["b.bias"], False, 0.0, 1e-3)
+    got = x * s.view(1, 7, 1, 1) + t.view(1, 7, 1, 1)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_combined_model_task_api(state_dict):
+    m = CombinedModel()
+    assert m.current_task == "person_detection"
+    for t in arch.TASKS:
+        m.set_task(t)
+        assert m.current_task == t
+    with pytest.raises(ValueError, match="not supported"):
+        m.set_task("segmentation")
+    with pytest.raises(KeyError):
+        m.load_state_dict({"foo": torch.zeros(1)})
+
+
+def test_synth_is_deterministic():
+    a = synth.uniform(3, "x", (1000,))
+    b = synth.uniform(3, "x", (1000,))
+    c = synth.uniform(4, "x", (1000,))
+    assert torch.equal(a, b) and not torch.equal(a, c)
+    assert float(a.min()) >= 0.0 and float(a.max()) < 1.0

@@ -1,0 +1,121 @@
+"""GPU: the full HIP hot path (prpe.CombinedModel) against the reference's golden outputs on
+the same seeded frames/weights (bs=2, 640x640) and against the oracle.
+
+Tolerances (north_star): heatmaps and face embeddings within 1e-3 abs of the fp32 CPU
+reference; norms within 1e-3 relative; detection tensor within 1e-3 abs on cls scores
+and 2e-3 x max|box| on pixel box coordinates (stride-8..32 scaled); keypoint
+OKS delta <= 1e-3; NMS on our own det output is bit-exact vs the oracle NMS of the same
+tensor, and the end-to-end match rate vs the reference's NMS is reported.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_ref as R
+from prpe import CombinedModel, synth
+from prpe.postproc import keypoints_from_heatmaps, non_max_suppression
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def model(state_dict):
+    return CombinedModel(state_dict, device="cuda")
+
+
+@pytest.fixture(scope="module")
+def frames():
+    return synth.frames(2).cuda()
+
+
+def test_face_detection_zero_stride_quirk(model, frames, golden_model):
+    model.set_task("face_detection")
+    det = model(frames).cpu().numpy()
+    ref = golden_model["det_face_s0"]
+    assert det.shape == ref.shape == (2, 5, 525)
+    assert np.all(det[:, :4] == 0)                       # Head.stride zeros -> boxes 0
+    np.testing.assert_allclose(det[:, 4], ref[:, 4], rtol=0, atol=1e-3)
+
+
+def test_person_detection_branch(model, frames, golden_model):
+    model.set_task("person_detection")
+    det = model(frames).cpu().numpy()
+    np.testing.assert_allclose(det[:, 4], golden_model["det_person_s0"][:, 4], rtol=0, atol=1e-3)
+
+
+def test_face_detection_with_strides(model, frames, golden_model):
+    model.set_task("face_detection")
+    model.yolo_face.yolo.head.stride = torch.tensor([8.0, 16.0, 32.0])
+    try:
+        det = model(frames).cpu().numpy()
+    finally:
+        model.yolo_face.yolo.head.stride = torch.zeros(3)
+    ref = golden_model["det_face_s8"]
+    np.testing.assert_allclose(det[:, 4], ref[:, 4], rtol=0, atol=1e-3)
+    # pixel boxes (DFL expectation x stride 8..32) amplify logit rounding: even an all-fp32-
+    # faithful run (precision=2 everywhere) differs by 0.48 px on ~930 px coordinates
+    # (tools/precision_sweep.py); tolerance 2e-3 x the largest coordinate (~1.9 px)
+    np.testing.assert_allclose(det[:, :4], ref[:, :4], rtol=0, atol=2e-3 * np.abs(ref[:, :4]).max())
+
+
+def test_pose_heatmaps_and_keypoints(model, frames, golden_model):
+    model.set_task("pose_estimation")
+    out = model(frames)
+    hm = out.heatmaps
+    ref = golden_model["heatmaps"]
+    err = np.abs(hm.cpu().numpy() - ref).max()
+    assert err <= 1e-3, err
+    c, s = keypoints_from_heatmaps(hm)
+    cr, sr = R.keypoints_from_heatmaps(torch.from_numpy(ref))
+    assert R.oks_delta(c.cpu(), cr) <= 1e-3
+    np.testing.assert_allclose(s.cpu().numpy(), sr.numpy(), rtol=1e-3)
+
+
+def test_face_recognition_embeddings(model, frames, golden_model):
+    model.set_task("face_recognition")
+    emb, norm = model(frames)
+    e = np.abs(emb.cpu().numpy() - golden_model["emb"]).max()
+    assert e <= 1e-3, e
+    np.testing.assert_allclose(norm.cpu().numpy(), golden_model["norm"], rtol=1e-3)
+    np.testing.assert_allclose(np.linalg.norm(emb.cpu().numpy(), axis=1), 1.0, rtol=1e-5)
+
+
+def test_forward_all_matches_per_task(model, frames, golden_model):
+    o = model.forward_all(frames, face_stride=[8.0, 16.0, 32.0])
+    assert np.abs(o["heatmaps"].cpu().numpy() - golden_model["heatmaps"]).max() <= 1e-3
+    assert np.abs(o["emb"].cpu().numpy() - golden_model["emb"]).max() <= 1e-3
+    np.testing.assert_allclose(o["det"].cpu().numpy()[:, 4], golden_model["det_face_s8"][:, 4], atol=1e-3)
+
+
+def test_nms_on_model_output_bit_exact_vs_oracle(model, frames, golden_model):
+    o = model.forward_all(frames, face_stride=[8.0, 16.0, 32.0])
+    det = o["det"]
+    ours = non_max_suppression(det)
+    theirs = R.non_max_suppression(det.cpu())
+    for a, b in zip(ours, theirs):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.numpy())
+    # end-to-end agreement with the reference's NMS on the reference's own det tensor: NMS is
+    # discontinuous in its inputs, so report the fraction of reference detections that have a
+    # same-class match (IoU >= 0.9, |score diff| < 1e-3) among ours (hard parts)
+    ref = R.non_max_suppression(torch.from_numpy(golden_model["det_face_s8"]))
+    rates = [nms_match_rate(a.cpu(), b) for a, b in zip(ours, ref)]
+    print("end-to-end NMS detection match rate vs reference:", rates)
+    assert min(rates) >= 0.9
+
+
+def _iou(a, b):
+    lt = torch.max(a[:, None, :2], b[None, :, :2])
+    rb = torch.min(a[:, None, 2:4], b[None, :, 2:4])
+    inter = (rb - lt).clamp(min=0).prod(-1)
+    area = lambda t: (t[:, 2] - t[:, 0]) * (t[:, 3] - t[:, 1])
+    return inter / (area(a)[:, None] + area(b)[None, :] - inter)
+
+
+def nms_match_rate(ours, ref):
+    if len(ref) == 0:
+        return 1.0 if len(ours) == 0 else 0.0
+    if len(ours) == 0:
+        return 0.0
+    iou = _iou(ref, ours)
+    ok = (iou >= 0.9) & ((ref[:, None, 4] - ours[None, :, 4]).abs() < 1e-3) & (ref[:, None, 5] == ours[None, :, 5])
+    return float(ok.any(1).float().mean())

@@ -1,0 +1,357 @@
+"""GPU: every HIP kernel of the hot path against a plain PyTorch fp32 CPU reference of the
+same op (floating-point kernels), at the shapes/variants the model uses.
+
+Tolerances (stated per test): the conv/GEMM path computes in split-bf16 x3 MFMA with fp32
+accumulation, i.e. each product to ~2^-17 relative; we allow |d| <= 2e-5 * (sum |a*b|)
+scale via rtol/atol on O(1) data. Memory-bound kernels are fp32 VALU: ~1e-6.
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from prpe import ops, pack
+from prpe._lib import RES_POST, RES_PRE
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _g(seed):
+    g = torch.Generator().manual_seed(seed)
+    return g
+
+
+def rnd(*shape, seed=0, scale=1.0):
+    return (torch.rand(*shape, generator=_g(seed)) * 2 - 1) * scale
+
+
+def act_ref(v, act, slope=None):
+    if act == "relu":
+        return F.relu(v)
+    if act == "silu":
+        return F.silu(v)
+    if act == "gelu":
+        return F.gelu(v)
+    if act == "prelu":
+        return F.prelu(v, slope)
+    if act == "sigmoid":
+        return torch.sigmoid(v)
+    return v
+
+
+def run_conv(x_nchw, w, stride, pad, act="none", scale=None, bias=None, slope=None, in_s=None, in_b=None,
+             res=None, res_mode=0, precision=0, tile=0, x_layout="nhwc"):
+    co = w.shape[0]
+    p = pack.pack_conv("t", w, stride, pad, DEV, scale=scale, bias=bias, slope=slope, in_scale=in_s,
+                       in_bias=in_b, act=act)
+    if x_layout == "nchw":
+        xd = ops.nhwc(x_nchw.to(DEV))
+    else:
+        xd = x_nchw.permute(0, 2, 3, 1).contiguous().to(DEV)
+    B, _, H, W = x_nchw.shape
+    Ho = (H + 2 * pad - w.shape[2]) // stride + 1
+    Wo = (W + 2 * pad - w.shape[3]) // stride + 1
+    y = torch.empty(B, Ho, Wo, co, device=DEV)
+    r = res.permute(0, 2, 3, 1).contiguous().to(DEV) if res is not None else None
+    ops.conv2d(xd, p, y, res=r, res_mode=res_mode, precision=precision, tile=tile)
+    torch.cuda.synchronize()
+    return y.permute(0, 3, 1, 2).cpu()
+
+
+def ref_conv(x, w, stride, pad, act="none", scale=None, bias=None, slope=None, in_s=None, in_b=None, res=None,
+             res_mode=0):
+    xx = x.double()
+    if in_s is not None:
+        xx = xx * in_s.double().view(1, -1, 1, 1) + in_b.double().view(1, -1, 1, 1)
+    v = F.conv2d(xx, w.double(), None, stride, pad)
+    if scale is not None:
+        v = v * scale.double().view(1, -1, 1, 1)
+    if bias is not None:
+        v = v + bias.double().view(1, -1, 1, 1)
+    if res_mode == RES_PRE:
+        v = v + res.double()
+    v = act_ref(v.float(), act, slope).double()
+    if res_mode == RES_POST:
+        v = v + res.double()
+    return v.float()
+
+
+def _tol(x, w):
+    # bound ~ 2^-16 * sum|x||w| per output; O(1) data -> use a scale-aware atol
+    k = w[0].numel()
+    return 4e-5 * math.sqrt(k) + 1e-6
+
+
+@pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", [
+    (2, 64, 20, 20, 256, 1, 1, 0),      # 1x1
+    (2, 64, 17, 19, 96, 3, 1, 1),       # 3x3 ragged spatial, ragged Co
+    (2, 32, 20, 20, 64, 3, 2, 1),       # 3x3 / 2
+    (1, 256, 10, 10, 512, 1, 2, 0),     # 1x1 / 2 (downsample)
+    (2, 8, 40, 40, 16, 3, 1, 1),        # Ci = 8 (YOLO Residual)
+    (2, 48, 12, 12, 64, 1, 1, 0),       # Ci = 48 (CSP conv2)
+    (1, 512, 7, 7, 64, 7, 1, 0),        # IR-50 output linear as 7x7 conv
+])
+def test_conv_vector_path(B, Ci, H, W, Co, k, s, p):
+    x = rnd(B, Ci, H, W, seed=1)
+    w = rnd(Co, Ci, k, k, seed=2, scale=1.0 / math.sqrt(Ci * k * k))
+    got = run_conv(x, w, s, p)
+    ref = ref_conv(x, w, s, p)
+    torch.testing.assert_close(got, ref, rtol=0, atol=_tol(x, w))
+
+
+@pytest.mark.parametrize("B,H,W,Co,k,s,p", [
+    (2, 64, 64, 64, 7, 2, 3),           # ResNet stem (NCHW input, Ci = 3)
+    (2, 40, 40, 16, 3, 2, 1),           # YOLO p1
+    (2, 64, 48, 768, 16, 16, 2),        # ViT patch embed (k16 s16 pad 2)
+])
+def test_conv_scalar_path_nchw_input(B, H, W, Co, k, s, p):
+    x = rnd(B, 3, H, W, seed=3)
+    w = rnd(Co, 3, k, k, seed=4, scale=1.0 / math.sqrt(3 * k * k))
+    got = run_conv(x, w, s, p, x_layout="nchw")
+    ref = ref_conv(x, w, s, p)
+    torch.testing.assert_close(got, ref, rtol=0, atol=_tol(x, w))
+
+
+@pytest.mark.parametrize("act", ["relu", "silu", "gelu", "prelu", "sigmoid"])
+def test_conv_epilogue_acts_and_affine(act):
+    Ci, Co = 32, 40
+    x = rnd(2, Ci, 9, 11, seed=5)
+    w = rnd(Co, Ci, 3, 3, seed=6, scale=0.1)
+    sc = torch.rand(Co, generator=_g(7)) + 0.5
+    bi = rnd(Co, seed=8)
+    sl = torch.rand(Co, generator=_g(9)) * 0.4
+    got = run_conv(x, w, 1, 1, act=act, scale=sc, bias=bi, slope=sl if act == "prelu" else None)
+    ref = ref_conv(x, w, 1, 1, act=act, scale=sc, bias=bi, slope=sl)
+    torch.testing.assert_close(got, ref, rtol=0, atol=2e-4)
+
+
+@pytest.mark.parametrize("mode", [RES_PRE, RES_POST])
+def test_conv_residual_modes(mode):
+    x = rnd(2, 64, 10, 10, seed=10)
+    w = rnd(64, 64, 3, 3, seed=11, scale=0.05)
+    r = rnd(2, 64, 10, 10, seed=12)
+    got = run_conv(x, w, 1, 1, act="relu", res=r, res_mode=mode)
+    ref = ref_conv(x, w, 1, 1, act="relu", res=r, res_mode=mode)
+    torch.testing.assert_close(got, ref, rtol=0, atol=2e-4)
+
+
+def test_conv_prologue_affine_zero_padding():
+    """IR-50 pre-BN: affine applied to in-bounds taps only; padding stays 0 (net_adaface.py:159)."""
+    x = rnd(2, 64, 8, 8, seed=13)
+    w = rnd(32, 64, 3, 3, seed=14, scale=0.05)
+    s = torch.rand(64, generator=_g(15)) + 0.5
+    b = rnd(64, seed=16)
+    got = run_conv(x, w, 1, 1, in_s=s, in_b=b)
+    ref = ref_conv(x, w, 1, 1, in_s=s, in_b=b)
+    torch.testing.assert_close(got, ref, rtol=0, atol=2e-4)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+def test_conv_every_tile_config(tile):
+    x = rnd(2, 64, 9, 13, seed=17)
+    w = rnd(150, 64, 3, 3, seed=18, scale=0.05)
+    got = run_conv(x, w, 1, 1, tile=tile)
+    ref = ref_conv(x, w, 1, 1)
+    torch.testing.assert_close(got, ref, rtol=0, atol=2e-4)
+
+
+def test_conv_strided_views_in_and_out():
+    """Input = channel slice of a concat buffer, output written into another slice."""
+    big = rnd(2, 10, 10, 96, seed=19).to(DEV)
+    xin = big[..., 32:96]                      # 64 channels, channel stride 1, pixel stride 96
+    w = rnd(24, 64, 3, 3, seed=20, scale=0.05)
+    p = pack.pack_conv("t", w, 1, 1, DEV)
+    out = torch.zeros(2, 10, 10, 80, device=DEV)
+    ops.conv2d(xin, p, out[..., 40:64])
+    torch.cuda.synchronize()
+    ref = ref_conv(xin.cpu().permute(0, 3, 1, 2), w, 1, 1)
+    torch.testing.assert_close(out[..., 40:64].cpu().permute(0, 3, 1, 2), ref, rtol=0, atol=2e-4)
+    assert torch.all(out[..., :40] == 0) and torch.all(out[..., 64:] == 0)
+
+
+def test_conv_precision_modes_ordering():
+    """plain bf16 >> 2-plane split (~2^-17) >> 3-plane split (fp32-faithful, ~fp32 rounding)."""
+    x = rnd(1, 256, 16, 16, seed=21)
+    w = rnd(128, 256, 3, 3, seed=22, scale=0.02)
+    ref = ref_conv(x, w, 1, 1)                      # fp64 accumulate
+    e3 = (run_conv(x, w, 1, 1, precision=0) - ref).abs().max().item()
+    e1 = (run_conv(x, w, 1, 1, precision=1) - ref).abs().max().item()
+    e6 = (run_conv(x, w, 1, 1, precision=2) - ref).abs().max().item()
+    f32 = (F.conv2d(x, w, None, 1, 1) - ref).abs().max().item()   # CPU fp32 itself
+    assert e3 < e1 / 50, (e3, e1)
+    assert e6 < e3, (e6, e3)
+    # fp32 accumulation of K = 2304 terms in one MFMA accumulator: ~sqrt(K)*2^-24*|y|
+    # (mkldnn's blocked fp32 sums are ~6x tighter on this shape)
+    assert e6 <= 10 * f32 + 1e-6, (e6, f32)
+
+
+@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+def test_conv_fp32_faithful_mode_every_tile(tile):
+    x = rnd(2, 64, 9, 13, seed=46)
+    w = rnd(150, 64, 3, 3, seed=47, scale=0.05)
+    got = run_conv(x, w, 1, 1, precision=2, tile=tile, act="relu")
+    ref = ref_conv(x, w, 1, 1, act="relu")
+    torch.testing.assert_close(got, ref, rtol=0, atol=2e-6)
+
+
+def test_conv_fp32_faithful_stem_scalar_path():
+    x = rnd(2, 3, 48, 48, seed=48)
+    w = rnd(64, 3, 7, 7, seed=49, scale=0.1)
+    got = run_conv(x, w, 2, 3, precision=2, x_layout="nchw")
+    ref = ref_conv(x, w, 2, 3)
+    torch.testing.assert_close(got, ref, rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("hi,wi,ho,wo,ac,act", [(20, 20, 160, 160, True, "silu"), (20, 20, 112, 112, True, "prelu"),
+                                               (20, 20, 256, 192, True, "gelu"), (16, 12, 64, 48, False, "none")])
+def test_upconv_equals_upsample_then_conv(hi, wi, ho, wo, ac, act):
+    Ci, Co = 32, 24
+    x = rnd(2, Ci, hi, wi, seed=23)
+    w = rnd(Co, Ci, 3, 3, seed=24, scale=0.05)
+    sc = torch.rand(Co, generator=_g(25)) + 0.5
+    bi = rnd(Co, seed=26)
+    sl = torch.rand(Co, generator=_g(27)) * 0.4
+    taps = pack.pack_upconv_taps("t", w, DEV)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    z = torch.empty(2, hi, wi, 9 * Co, device=DEV)
+    ops.conv2d(xd, taps, z)
+    y = torch.empty(2, ho, wo, Co, device=DEV)
+    ops.upconv3x3(z, y, ac, sc.to(DEV), bi.to(DEV), sl.to(DEV) if act == "prelu" else None, act)
+    torch.cuda.synchronize()
+    u = F.interpolate(x.double(), size=(ho, wo), mode="bilinear", align_corners=ac)
+    ref = F.conv2d(u, w.double(), None, 1, 1) * sc.double().view(1, -1, 1, 1) + bi.double().view(1, -1, 1, 1)
+    ref = act_ref(ref.float(), act, sl)
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=2e-4)
+
+
+def test_upconv_nchw_output_view():
+    x = rnd(1, 16, 16, 12, seed=28)
+    w = rnd(17, 16, 3, 3, seed=29, scale=0.1)
+    bi = rnd(17, seed=30)
+    taps = pack.pack_upconv_taps("t", w, DEV)
+    z = torch.empty(1, 16, 12, 9 * 17, device=DEV)
+    ops.conv2d(x.permute(0, 2, 3, 1).contiguous().to(DEV), taps, z)
+    heat = torch.empty(1, 17, 64, 48, device=DEV)
+    ops.upconv3x3(z, ops.nhwc(heat), False, None, bi.to(DEV), None, "none")
+    torch.cuda.synchronize()
+    ref = F.conv2d(F.interpolate(x, scale_factor=4.0, mode="bilinear", align_corners=False), w, bi, 1, 1)
+    torch.testing.assert_close(heat.cpu(), ref, rtol=0, atol=1e-4)
+
+
+def test_dwconv_with_residual():
+    x = rnd(2, 80, 10, 10, seed=31)
+    w = rnd(80, 1, 3, 3, seed=32)
+    sc = torch.rand(80, generator=_g(33)) + 0.5
+    bi = rnd(80, seed=34)
+    r = rnd(2, 80, 10, 10, seed=35)
+    y = torch.empty(2, 10, 10, 80, device=DEV)
+    ops.dwconv(x.permute(0, 2, 3, 1).contiguous().to(DEV), y, w.reshape(-1).to(DEV), 3, 1, 1, sc.to(DEV), bi.to(DEV),
+               "silu", res=r.permute(0, 2, 3, 1).contiguous().to(DEV))
+    torch.cuda.synchronize()
+    ref = F.silu(F.conv2d(x, w, None, 1, 1, 1, 80) * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)) + r
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=1e-5)
+
+
+@pytest.mark.parametrize("k,s,p,H", [(3, 2, 1, 33), (5, 1, 2, 5), (1, 2, 0, 14)])
+def test_maxpool(k, s, p, H):
+    x = rnd(2, 16, H, H, seed=36)
+    Ho = (H + 2 * p - k) // s + 1
+    y = torch.empty(2, Ho, Ho, 16, device=DEV)
+    ops.maxpool(x.permute(0, 2, 3, 1).contiguous().to(DEV), y, k, s, p)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), F.max_pool2d(x, k, s, p), rtol=0, atol=0)
+
+
+def test_upsample_nearest2x():
+    x = rnd(2, 8, 5, 5, seed=37)
+    y = torch.empty(2, 10, 10, 8, device=DEV)
+    ops.upsample_nearest2x(x.permute(0, 2, 3, 1).contiguous().to(DEV), y)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), F.interpolate(x, scale_factor=2.0, mode="nearest"),
+                               rtol=0, atol=0)
+
+
+def test_norm_sigmoid():
+    x = rnd(3, 3, 40, 40, seed=38, scale=3.0) + 0.7
+    y = torch.empty(3, 40, 40, 3, device=DEV)
+    ops.norm_sigmoid(x.permute(0, 2, 3, 1).contiguous().to(DEV), y)
+    torch.cuda.synchronize()
+    r = x - x.mean(dim=(2, 3), keepdim=True)
+    r = torch.sigmoid(r / (r.std(dim=(2, 3), keepdim=True) + 1e-6))
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), r, rtol=0, atol=2e-6)
+
+
+@pytest.mark.parametrize("relu", [False, True])
+def test_layernorm(relu):
+    x = rnd(384, 768, seed=39, scale=4.0) + 1.0
+    g = torch.rand(768, generator=_g(40)) + 0.5
+    b = rnd(768, seed=41)
+    y = torch.empty(384, 768, device=DEV)
+    ops.layernorm(x.to(DEV), y, g.to(DEV), b.to(DEV), 1e-12, relu)
+    torch.cuda.synchronize()
+    ref = F.layer_norm(x, (768,), g, b, 1e-12)
+    if relu:
+        ref = F.relu(ref)
+    torch.testing.assert_close(y.cpu(), ref, rtol=0, atol=1e-5)
+
+
+def test_vit_attention():
+    B, L, H, D = 3, 192, 12, 64
+    qkv = rnd(B * L, 3 * H * D, seed=42, scale=2.0)
+    out = torch.empty(B * L, H * D, device=DEV)
+    ops.attention(qkv.to(DEV), out, B, L, H, D, D ** -0.5)
+    torch.cuda.synchronize()
+    q, k, v = qkv.view(B, L, 3, H, D).permute(2, 0, 3, 1, 4).double()
+    att = torch.softmax(q @ k.transpose(-1, -2) * D ** -0.5, -1)
+    ref = (att @ v).transpose(1, 2).reshape(B * L, H * D).float()
+    torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=5e-5)
+
+
+def test_psa_attention():
+    B, nh, dk, dh = 2, 2, 32, 64
+    per = 2 * dk + dh
+    qkv = rnd(B, nh * per, 5, 5, seed=43)
+    out = torch.empty(B, 5, 5, nh * dh, device=DEV)
+    vout = torch.empty(B, 5, 5, nh * dh, device=DEV)
+    ops.psa_attention(qkv.permute(0, 2, 3, 1).contiguous().to(DEV), out, vout, nh, dk, dh, dk ** -0.5)
+    torch.cuda.synchronize()
+    t = qkv.view(B, nh, per, 25)
+    q, k, v = t.split([dk, dk, dh], dim=2)
+    att = ((q.transpose(-2, -1) @ k) * dk ** -0.5).softmax(-1)
+    ref = (v @ att.transpose(-2, -1)).reshape(B, nh * dh, 5, 5)
+    torch.testing.assert_close(out.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=1e-5)
+    torch.testing.assert_close(vout.permute(0, 3, 1, 2).cpu(), v.reshape(B, nh * dh, 5, 5), rtol=0, atol=0)
+
+
+def test_l2norm():
+    x = rnd(37, 512, seed=44, scale=5.0)
+    emb = torch.empty(37, 512, device=DEV)
+    nrm = torch.empty(37, 1, device=DEV)
+    ops.l2norm(x.to(DEV), emb, nrm)
+    torch.cuda.synchronize()
+    n = torch.norm(x, 2, 1, True)
+    torch.testing.assert_close(nrm.cpu(), n, rtol=1e-6, atol=0)
+    torch.testing.assert_close(emb.cpu(), x / n, rtol=0, atol=1e-7)
+
+
+@pytest.mark.parametrize("stride", [(0.0, 0.0, 0.0), (8.0, 16.0, 32.0)])
+def test_dfl_decode_matches_oracle_head(stride):
+    from oracle.model_ref import make_anchors
+    B, A = 2, 525
+    head = rnd(B, A, 65, seed=45, scale=3.0)
+    det = torch.empty(B, 5, A, device=DEV)
+    ops.dfl_decode(head.to(DEV), det, 1, [(20, 20), (10, 10), (5, 5)], stride)
+    torch.cuda.synchronize()
+    # oracle decode (nn.py:261-270)
+    feats = [torch.zeros(B, 65, h, h) for h in (20, 10, 5)]
+    anchors, strides = (t.transpose(0, 1) for t in make_anchors(feats, stride))
+    x = head.transpose(1, 2)
+    box, cls = x.split((64, 1), 1)
+    d = box.reshape(B, 4, 16, A).transpose(2, 1).softmax(1)
+    d = F.conv2d(d, torch.arange(16, dtype=torch.float32).view(1, 16, 1, 1)).view(B, 4, A)
+    lt, rb = d.chunk(2, 1)
+    a1, b1 = anchors.unsqueeze(0) - lt, anchors.unsqueeze(0) + rb
+    ref = torch.cat((torch.cat(((a1 + b1) / 2, b1 - a1), 1) * strides, cls.sigmoid()), 1)
+    torch.testing.assert_close(det.cpu(), ref, rtol=2e-6, atol=2e-5)

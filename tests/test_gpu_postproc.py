@@ -1,0 +1,111 @@
+"""GPU: NMS and soft-argmax kernels against the reference's own outputs (golden vectors made
+by the reference code, oracle/make_golden.py) and the oracle, incl. edge cases.
+
+Bar: NMS bit-exact (indices/rows/counts) on identical inputs; soft-argmax coords within
+1e-6 abs, scores 1e-6 rel, hard-argmax index exact.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+
+from oracle import model_ref as R
+from prpe import ops
+from prpe.postproc import keypoints_from_heatmaps, non_max_suppression, non_max_suppression_padded
+
+pytestmark = pytest.mark.gpu
+
+
+def _load(name):
+    with np.load(os.path.join(GOLDEN, name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def _rows_sorted(a):
+    return a[np.lexsort(a.T[::-1])] if len(a) else a
+
+
+@pytest.mark.parametrize("case", ["det", "evalstep", "stress"])
+def test_nms_matches_reference_golden(case):
+    g = _load("golden_nms.npz")
+    inp = torch.from_numpy(g[f"{case}_in"]).cuda()
+    out, cnt = non_max_suppression_padded(inp)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(cnt.cpu().numpy(), g[f"{case}_count"])
+    got = out.cpu().numpy()
+    for i, n in enumerate(g[f"{case}_count"]):
+        a, b = got[i, :n], g[f"{case}_out"][i, :n]
+        if case == "evalstep":    # multi-label path, tie order unspecified upstream
+            a, b = _rows_sorted(a), _rows_sorted(b)
+        np.testing.assert_array_equal(a, b)
+        assert np.all(got[i, n:] == 0)
+
+
+def test_nms_list_api_and_transposed_layout():
+    g = _load("golden_nms.npz")
+    inp = torch.from_numpy(g["det_in"]).cuda()
+    dets = non_max_suppression(inp)
+    out1, cnt1 = ops.nms(inp.transpose(1, 2).contiguous(), 1)      # [B, N, 4+nc] layout
+    torch.cuda.synchronize()
+    for i, d in enumerate(dets):
+        np.testing.assert_array_equal(d.cpu().numpy(), g["det_out"][i, :g["det_count"][i]])
+        np.testing.assert_array_equal(out1[i, :cnt1[i]].cpu().numpy(), d.cpu().numpy())
+
+
+def test_nms_ties_are_stable_by_index():
+    # 4 identical boxes, identical scores, far apart classes -> all kept, in index order
+    b, n = 1, 6
+    x = torch.zeros(b, 5, n)
+    x[0, 0] = torch.tensor([10., 10., 10., 100., 200., 300.])
+    x[0, 1] = 10.0
+    x[0, 2:4] = 4.0
+    x[0, 4] = torch.tensor([0.5, 0.5, 0.5, 0.5, 0.5, 0.5])
+    out, cnt = non_max_suppression_padded(x.cuda())
+    ref = R.non_max_suppression(x)[0]
+    assert int(cnt[0]) == ref.shape[0] == 4
+    np.testing.assert_array_equal(out[0, :4].cpu().numpy(), ref.numpy())
+
+
+def test_nms_empty_and_all_below_threshold():
+    x = torch.zeros(3, 5, 50)
+    x[:, 2:4] = 5.0
+    x[1, 4] = 0.0005                     # below conf 0.001
+    x[2, 4, 7] = float("nan")            # NaN never a candidate
+    out, cnt = non_max_suppression_padded(x.cuda())
+    assert cnt.tolist() == [0, 0, 0]
+    assert torch.all(out == 0)
+
+
+def test_nms_max_det_cap_and_multilabel():
+    torch.manual_seed(0)
+    x = torch.rand(2, 4 + 3, 400)
+    x[:, 0:2] *= 600
+    x[:, 2:4] = x[:, 2:4] * 20 + 2
+    out, cnt = non_max_suppression_padded(x.cuda())
+    ref = R.non_max_suppression(x)
+    for i, r in enumerate(ref):
+        assert int(cnt[i]) == r.shape[0] == 300
+        np.testing.assert_array_equal(out[i, :300].cpu().numpy(), r.numpy())
+
+
+@pytest.mark.parametrize("case,boxes", [("model", False), ("peaky", True)])
+def test_softargmax_matches_reference_golden(case, boxes):
+    g = _load("golden_softargmax.npz")
+    hm = torch.from_numpy(g[f"{case}_in"]).cuda()
+    bx = torch.from_numpy(g["peaky_boxes"]).cuda() if boxes else None
+    c, s = keypoints_from_heatmaps(hm, bx)
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(c.cpu().numpy(), g[f"{case}_coords"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(s.cpu().numpy(), g[f"{case}_scores"], rtol=2e-6, atol=0)
+
+
+def test_softargmax_hard_argmax_index_exact():
+    g = _load("golden_softargmax.npz")
+    hm = torch.from_numpy(g["peaky_in"])
+    _, _, am = ops.softargmax(hm.cuda(), None, want_argmax=True)
+    torch.cuda.synchronize()
+    ref = hm.reshape(hm.shape[0], hm.shape[1], -1).argmax(-1).int()
+    assert torch.equal(am.cpu(), ref)
