@@ -73,6 +73,7 @@ def main():
     dev = torch.device("cuda", local)
     from prpe import CombinedModel, arch, synth
     from prpe.postproc import non_max_suppression_padded
+    from prpe.dist import gather_detections
     from prpe import ops
 
     prec = args.precision if args.precision == "auto" else int(args.precision)
@@ -89,10 +90,7 @@ def main():
         dets, cnt = non_max_suppression_padded(o["det"])
         coords, scores = ops.softargmax(o["heatmaps"])
         if ws > 1:
-            gd = torch.empty((ws,) + tuple(dets.shape), device=dev)
-            gc = torch.empty((ws,) + tuple(cnt.shape), device=dev, dtype=cnt.dtype)
-            dist.all_gather_into_tensor(gd, dets)
-            dist.all_gather_into_tensor(gc, cnt)
+            gather_detections(dets, cnt)          # RCCL all-gather over xGMI (prpe/dist.py)
         return o, coords
 
     for _ in range(args.warmup):
