@@ -96,10 +96,14 @@ int prpe_conv2d(const prpe_conv_desc* d, void* stream);
  * align_corners = 1: src = dst*(in-1)/(out-1);  0: src = max(0,(dst+0.5)*in/out-0.5).
  * Replaces nn.Upsample(bilinear) + Conv2d(3x3) + BN + act in modify_models.py:47-52,
  * :237-242, :359-364 and the ViTPose simple decoder (modeling_vitpose.py:120-144).
+ * With a workspace of >= prpe_upconv3x3_workspace_bytes(z, y) bytes the sum is evaluated
+ * separably (x-interpolation into the workspace, then y; 6 loads per output instead of
+ * 36); workspace = NULL selects the direct one-pass kernel.
  */
+int64_t prpe_upconv3x3_workspace_bytes(const prpe_view* z, const prpe_view* y);
 int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,
                    const float* scale, const float* bias, const float* slope, int32_t act,
-                   void* stream);
+                   void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Depthwise kxk conv (groups = C) + folded BN + act (+ post-act residual add when res.ptr).
  * Replaces yolopt Conv(g=ch) (nn.py:108, :248-250). */
@@ -111,6 +115,10 @@ int prpe_dwconv(const prpe_view* x, const prpe_view* y, const prpe_view* res,
  * yolopt SPP (nn.py:88-94), IR-50 MaxPool2d(1, s) shortcut (net_adaface.py:148). */
 int prpe_maxpool(const prpe_view* x, const prpe_view* y, int32_t k, int32_t stride,
                  int32_t pad, void* stream);
+
+/* Strided copy with channel zero-padding: y[...,c] = c < x.c ? x[...,c] : 0 (e.g. NCHW frames
+ * -> NHWC4 for the vectorised stem conv; the 4th channel meets a zero weight column). */
+int prpe_copy_pad(const prpe_view* x, const prpe_view* y, void* stream);
 
 /* Nearest x2 upsample (yolopt DarkFPN nn.Upsample(scale_factor=2), nn.py:195). */
 int prpe_upsample_nearest2x(const prpe_view* x, const prpe_view* y, void* stream);

@@ -36,14 +36,17 @@ struct ConvK {
   const uint16_t* whi; const uint16_t* wlo; const uint16_t* wlo2;
   const float* scale; const float* bias; const float* slope;
   const float* in_scale; const float* in_bias;
-  int act, res_mode;
+  int act, res_mode, vec_out;
   int M, HoWo, tiles_n, nwg;
 };
 
-__device__ __forceinline__ int swzF(int row) {
-  const int q = (row >> 2) & 3;
-  return q == 0 ? 0 : q == 1 ? 2 : q == 2 ? 3 : 1;
-}
+// F = {0,2,3,1} indexed by (row >> 2) & 3, branch-free
+__device__ __forceinline__ int swzF(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
+
+// native vector types: HIP's float4/uint4 are structs, and arrays of them cannot be promoted
+// to registers (the compiler moved them to a per-thread LDS array with 64-B lane stride)
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 
 template <int BM, int BN, int WM, int WN, bool VEC, int PREC>
 __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
@@ -57,7 +60,10 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
   static_assert(TM >= 1 && TN >= 1, "tile");
 
   // LDS: [buf][plane][rows][32] bf16 (u16), A then B.
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * NP * (BM + BN) * BK];
+  // staging ring (2 buffers x NP planes x (A|B) tiles) re-used for the epilogue's C tile
+  constexpr int LDS_U16 = (2 * NP * (BM + BN) * BK) > (BM * (BN + 4) * 2) ? (2 * NP * (BM + BN) * BK)
+                                                                          : (BM * (BN + 4) * 2);
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
   __shared__ int klut[VEC ? 1 : 1024];
 
   const int tid = threadIdx.x;
@@ -117,28 +123,25 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
     while (c_ci >= p.Ci) { c_ci -= p.Ci; if (++c_kw == p.KW) { c_kw = 0; ++c_kh; } }
   }
 
-  float4 areg[VEC ? A_ROWS_PT : 1];
+  f4 areg[VEC ? A_ROWS_PT : 1];
   float sreg[VEC ? 1 : S_KPT];
-  uint4 breg[NP][B_PT];
+  u4 breg[NP][B_PT];
 
   auto load_tile = [&](int kt) {
     if constexpr (VEC) {
       const bool kval = c_kh < p.KH;
-      float4 s4 = make_float4(1.f, 1.f, 1.f, 1.f), b4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      f4 s4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
       if (p.in_scale && kval) {
-        s4 = *reinterpret_cast<const float4*>(p.in_scale + c_ci);
-        b4 = *reinterpret_cast<const float4*>(p.in_bias + c_ci);
+        s4 = *reinterpret_cast<const f4*>(p.in_scale + c_ci);
+        b4 = *reinterpret_cast<const f4*>(p.in_bias + c_ci);
       }
 #pragma unroll
       for (int i = 0; i < A_ROWS_PT; ++i) {
         const int ih = ih0[i] + c_kh, iw = iw0[i] + c_kw;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        f4 v = {0.f, 0.f, 0.f, 0.f};
         if (kval && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) {
-          v = *reinterpret_cast<const float4*>(p.x + rowoff[i] + ih * p.xsh + iw * p.xsw + c_ci);
-          if (p.in_scale) {
-            v.x = v.x * s4.x + b4.x; v.y = v.y * s4.y + b4.y;
-            v.z = v.z * s4.z + b4.z; v.w = v.w * s4.w + b4.w;
-          }
+          v = *reinterpret_cast<const f4*>(p.x + rowoff[i] + ih * p.xsh + iw * p.xsw + c_ci);
+          if (p.in_scale) v = v * s4 + b4;
         }
         areg[i] = v;
       }
@@ -171,9 +174,9 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
       if (B_CHUNKS % NTHREADS == 0 || c < B_CHUNKS) {
         const int row = c >> 2, ch = c & 3;
         const int64_t off = (int64_t)(n0 + row) * p.k_pad + kt * BK + ch * 8;
-        breg[0][j] = *reinterpret_cast<const uint4*>(p.whi + off);
-        if (NP > 1) breg[1][j] = *reinterpret_cast<const uint4*>(p.wlo + off);
-        if (NP > 2) breg[NP - 1][j] = *reinterpret_cast<const uint4*>(p.wlo2 + off);
+        breg[0][j] = *reinterpret_cast<const u4*>(p.whi + off);
+        if (NP > 1) breg[1][j] = *reinterpret_cast<const u4*>(p.wlo + off);
+        if (NP > 2) breg[NP - 1][j] = *reinterpret_cast<const u4*>(p.wlo2 + off);
       }
     }
   };
@@ -187,8 +190,8 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
         const int slot = (c4 >> 1) ^ swzF(row);
         const int off = row * BK + slot * 8 + (c4 & 1) * 4;
         bf16x4 pl[NP];
-        const float4 v = areg[i];
-        const float vv[4] = {v.x, v.y, v.z, v.w};
+        const f4 v = areg[i];
+        const float vv[4] = {v[0], v[1], v[2], v[3]};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float r = vv[e];
@@ -226,7 +229,7 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
         const int row = c >> 2, ch = c & 3;
         const int off = row * BK + (ch ^ swzF(row)) * 8;
 #pragma unroll
-        for (int q = 0; q < NP; ++q) *reinterpret_cast<uint4*>(B_at(buf, q) + off) = breg[q][j];
+        for (int q = 0; q < NP; ++q) *reinterpret_cast<u4*>(B_at(buf, q) + off) = breg[q][j];
       }
     }
   };
@@ -282,6 +285,50 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
   }
 
   // ---------------- epilogue
+  if (p.vec_out) {
+    // Stage the raw accumulator tile through LDS (free after the loop's last barrier), then
+    // every thread owns 16-B column chunks of whole rows: coalesced float4 residual loads and
+    // output stores (a wave moves 1 KB per instruction) instead of 64-B row fragments.
+    constexpr int CS = BN + 4;                      // padded row (floats)
+    float* ct = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ct[(wm * WTM + i * 16 + fg * 4 + r) * CS + wn * WTN + j * 16 + fr] = acc[i][j][r];
+    __syncthreads();
+    constexpr int CPR = BN / 4;                     // float4 chunks per tile row
+    constexpr int RPP = NTHREADS / CPR;             // rows per pass
+    const int cc = tid % CPR;
+    const int col = n0 + cc * 4;
+    if (col < p.Co) {
+      f4 sc4 = {1.f, 1.f, 1.f, 1.f}, bi4 = {0.f, 0.f, 0.f, 0.f}, sl4 = {0.f, 0.f, 0.f, 0.f};
+      if (p.scale) sc4 = *reinterpret_cast<const f4*>(p.scale + col);
+      if (p.bias) bi4 = *reinterpret_cast<const f4*>(p.bias + col);
+      if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
+      for (int rr = tid / CPR; rr < BM; rr += RPP) {
+        const int m = m0 + rr;
+        if (m >= p.M) break;
+        const int n = m / p.HoWo;
+        const int rem = m - n * p.HoWo;
+        const int oh = rem / p.Wo;
+        const int ow = rem - oh * p.Wo;
+        f4 v = *reinterpret_cast<const f4*>(ct + rr * CS + cc * 4);
+        v = v * sc4 + bi4;
+        f4 res = {0.f, 0.f, 0.f, 0.f};
+        if (p.res_mode != PRPE_RES_NONE)
+          res = *reinterpret_cast<const f4*>(p.r + (int64_t)n * p.rsn + (int64_t)oh * p.rsh + (int64_t)ow * p.rsw + col);
+        if (p.res_mode == PRPE_RES_PRE_ACT) v += res;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act, sl4[e]);
+        if (p.res_mode == PRPE_RES_POST_ACT) v += res;
+        *reinterpret_cast<f4*>(p.y + (int64_t)n * p.ysn + (int64_t)oh * p.ysh + (int64_t)ow * p.ysw + col) = v;
+      }
+    }
+    return;
+  }
   float sc[TN], bi[TN], sl[TN];
   int cols[TN];
 #pragma unroll
@@ -314,6 +361,81 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
         v = apply_act(v, p.act, sl[j]);
         if (p.res_mode == PRPE_RES_POST_ACT) v += p.r[ro + col * p.rsc];
         p.y[yo + col * p.ysc] = v;
+      }
+    }
+  }
+}
+
+// Direct fp32 conv for Co <= 4 (ViT adapter 128->3, YOLO adapter 64->3, head 80->1): a 16-wide
+// MFMA tile would waste >= 75 % of its columns and the layer is bound by reading its input.
+// Lanes run across input channels: a pixel is handled by LPP = pow2 >= Ci/4 lanes, each lane
+// owning 4 channels (one coalesced float4 per tap) and holding its slice of the weights for
+// all taps in registers (KHW*4*CO floats, rebuilt exactly as p0+p1+p2). Per pixel the LPP
+// partial dot products are combined with a shuffle tree; grid-stride over pixels.
+template <int CO, int KHW>
+__global__ __launch_bounds__(256) void conv_smallco_kernel(ConvK p, int lpp_log2) {
+  const int LPP = 1 << lpp_log2;
+  const int lane = threadIdx.x & 63;
+  const int c4 = lane & (LPP - 1);
+  const int slot = lane >> lpp_log2;
+  const int ppw = 64 >> lpp_log2;
+  const bool cval = c4 * 4 < p.Ci;
+  float w[KHW][4][CO];
+#pragma unroll
+  for (int t = 0; t < KHW; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int c = 0; c < CO; ++c) {
+        float v = 0.f;
+        if (cval) {
+          const int64_t o = (int64_t)c * p.k_pad + t * p.Ci + c4 * 4 + e;
+          v = (float)__builtin_bit_cast(__bf16, p.whi[o]) + (float)__builtin_bit_cast(__bf16, p.wlo[o]) +
+              (float)__builtin_bit_cast(__bf16, p.wlo2[o]);
+        }
+        w[t][e][c] = v;
+      }
+  const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int nw = (int)((gridDim.x * blockDim.x) >> 6);
+  for (int base = gw * ppw; base < p.M; base += nw * ppw) {
+    const int m = base + slot;
+    float acc[CO];
+#pragma unroll
+    for (int c = 0; c < CO; ++c) acc[c] = 0.f;
+    int n = 0, oh = 0, ow = 0;
+    if (m < p.M) {
+      n = m / p.HoWo;
+      const int rem = m - n * p.HoWo;
+      oh = rem / p.Wo;
+      ow = rem - oh * p.Wo;
+      const float* xb = p.x + (int64_t)n * p.xsn + c4 * 4;
+#pragma unroll
+      for (int t = 0; t < KHW; ++t) {
+        const int kh = KHW == 1 ? 0 : t / 3, kw = KHW == 1 ? 0 : t % 3;
+        const int ih = oh * p.stride - p.pad + kh, iw = ow * p.stride - p.pad + kw;
+        if (cval && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) {
+          const f4 v = *reinterpret_cast<const f4*>(xb + (int64_t)ih * p.xsh + (int64_t)iw * p.xsw);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+#pragma unroll
+            for (int c = 0; c < CO; ++c) acc[c] = fmaf(v[e], w[t][e][c], acc[c]);
+        }
+      }
+    }
+    for (int o = LPP >> 1; o > 0; o >>= 1)
+#pragma unroll
+      for (int c = 0; c < CO; ++c) acc[c] += __shfl_xor(acc[c], o, 64);
+    if (c4 == 0 && m < p.M) {
+      const int64_t yo = (int64_t)n * p.ysn + (int64_t)oh * p.ysh + (int64_t)ow * p.ysw;
+      const int64_t ro = (int64_t)n * p.rsn + (int64_t)oh * p.rsh + (int64_t)ow * p.rsw;
+#pragma unroll
+      for (int c = 0; c < CO; ++c) {
+        if (c >= p.Co) break;
+        float v = acc[c] * (p.scale ? p.scale[c] : 1.f) + (p.bias ? p.bias[c] : 0.f);
+        if (p.res_mode == PRPE_RES_PRE_ACT) v += p.r[ro + c * p.rsc];
+        v = apply_act(v, p.act, p.slope ? p.slope[c] : 0.f);
+        if (p.res_mode == PRPE_RES_POST_ACT) v += p.r[ro + c * p.rsc];
+        p.y[yo + c * p.ysc] = v;
       }
     }
   }
@@ -376,10 +498,39 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   kp.in_scale = d->in_scale; kp.in_bias = d->in_bias;
   kp.act = d->act; kp.res_mode = d->res_mode;
   kp.M = (int)M64; kp.HoWo = Ho * Wo;
+  auto a16 = [](const prpe_view& v) {
+    return v.sc == 1 && v.c % 4 == 0 && v.sw % 4 == 0 && v.sh % 4 == 0 && v.sn % 4 == 0 &&
+           ((uintptr_t)v.ptr % 16) == 0;
+  };
+  kp.vec_out = a16(y) && (d->res_mode == PRPE_RES_NONE || a16(d->res)) &&
+               (!d->scale || (uintptr_t)d->scale % 16 == 0) && (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
+               (!d->slope || (uintptr_t)d->slope % 16 == 0);
   hipStream_t st = as_stream(stream);
   const int prec = d->precision;
   int tile = d->tile;
-  if (tile == 0) tile = y.c > 64 ? 1 : y.c > 32 ? 2 : y.c > 16 ? 3 : 4;
+  // direct fp32 kernel for tiny Co (needs the 3 weight planes; exact fp32 products)
+  const int khw = d->kh * d->kw;
+  // (3x3 Co=3 stays on the MFMA path: measured 7.5 ms vs 11.8 ms for this kernel at bs=256)
+  if (tile == 0 && y.c <= 4 && vec && !d->in_scale && d->w_lo && d->w_lo2 && x.c <= 256 && khw == 1) {
+    int lg = 0;
+    while ((1 << lg) * 4 < x.c) ++lg;
+    const int ppb = 4 * (64 >> lg);                      // pixels per block-iteration
+    int blocks = (kp.M + ppb - 1) / ppb;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    if (y.c == 1) {
+      if (khw == 1) hipLaunchKernelGGL((conv_smallco_kernel<1, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
+      else hipLaunchKernelGGL((conv_smallco_kernel<1, 9>), dim3(blocks), dim3(256), 0, st, kp, lg);
+    } else if (y.c <= 3) {
+      if (khw == 1) hipLaunchKernelGGL((conv_smallco_kernel<3, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
+      else hipLaunchKernelGGL((conv_smallco_kernel<3, 9>), dim3(blocks), dim3(256), 0, st, kp, lg);
+    } else {
+      if (khw == 1) hipLaunchKernelGGL((conv_smallco_kernel<4, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
+      else hipLaunchKernelGGL((conv_smallco_kernel<4, 9>), dim3(blocks), dim3(256), 0, st, kp, lg);
+    }
+    return launch_status();
+  }
+  // measured (tools/conv_bench.py): 3-plane mode prefers 128x64 (LDS 72 KB -> 2 blocks/CU)
+  if (tile == 0) tile = (y.c > 64 && prec != 2) ? 1 : y.c > 32 ? 2 : y.c > 16 ? 3 : 4;
   switch (tile) {
     case 1: return launch_cfg<128, 128, 2, 2>(kp, vec, prec, st);
     case 2: return launch_cfg<128, 64, 2, 2>(kp, vec, prec, st);

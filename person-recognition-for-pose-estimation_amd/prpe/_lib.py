@@ -45,10 +45,12 @@ _F = C.c_float
 _VP = C.POINTER(View)
 SIGNATURES = {
     "prpe_conv2d": (C.c_int, [C.POINTER(ConvDesc), _P]),
-    "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _P]),
+    "prpe_upconv3x3_workspace_bytes": (C.c_int64, [_VP, _VP]),
+    "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _P, _L, _P]),
     "prpe_dwconv": (C.c_int, [_VP, _VP, _VP, _P, _I, _I, _I, _P, _P, _I, _P]),
     "prpe_maxpool": (C.c_int, [_VP, _VP, _I, _I, _I, _P]),
     "prpe_upsample_nearest2x": (C.c_int, [_VP, _VP, _P]),
+    "prpe_copy_pad": (C.c_int, [_VP, _VP, _P]),
     "prpe_norm_sigmoid": (C.c_int, [_VP, _VP, _P]),
     "prpe_layernorm": (C.c_int, [_P, _L, _P, _L, _L, _I, _P, _P, _F, _I, _P]),
     "prpe_attention": (C.c_int, [_P, _P, _I, _I, _I, _I, _F, _P]),

@@ -144,8 +144,18 @@ class Engine:
             return self._trunk(x_nchw)
 
     def _trunk(self, x_nchw):
-        x = ops.nhwc(x_nchw)
-        y = self.conv(x, self.pk("backbone.conv1", "backbone.conv1.weight", 2, 3, bn="backbone.bn1", act="relu"))
+        # NCHW frames -> NHWC4 (zero 4th channel) so the 7x7/2 stem runs the vectorised
+        # implicit-GEMM path; its weight gets a matching zero input channel
+        B0, _, H0, W0 = x_nchw.shape
+        x = ops.copy_pad(ops.nhwc(x_nchw), self.empty(B0, H0, W0, 4))
+        stem = self._packs.get("backbone.conv1")
+        if stem is None:
+            w = self.sd["backbone.conv1.weight"].float()
+            w4 = torch.cat([w, torch.zeros(w.shape[0], 1, *w.shape[2:])], 1)
+            s, b = bn_affine(self.sd, "backbone.bn1", BN_EPS)
+            stem = pack_conv("backbone.conv1", w4, 2, 3, self.device, scale=s, bias=b, act="relu")
+            self._packs["backbone.conv1"] = stem
+        y = self.conv(x, stem)
         B, H, W, C = y.shape
         mp = self.empty(B, (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1, C)
         x = ops.maxpool(y, mp, 3, 2, 1)

@@ -55,9 +55,14 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
     return y
 
 
-def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none"):
-    check(lib().prpe_upconv3x3(C.byref(view(z)), C.byref(view(y)), 1 if align_corners else 0,
-                               _ptr(scale), _ptr(bias), _ptr(slope), ACT[act], _stream()), "prpe_upconv3x3")
+def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none", separable=True):
+    zv, yv = view(z), view(y)
+    ws, nbytes = None, 0
+    if separable:
+        nbytes = lib().prpe_upconv3x3_workspace_bytes(C.byref(zv), C.byref(yv))
+        ws = torch.empty((nbytes + 3) // 4, device=z.device, dtype=torch.float32)
+    check(lib().prpe_upconv3x3(C.byref(zv), C.byref(yv), 1 if align_corners else 0, _ptr(scale), _ptr(bias),
+                               _ptr(slope), ACT[act], _ptr(ws), nbytes, _stream()), "prpe_upconv3x3")
     return y
 
 
@@ -69,6 +74,11 @@ def dwconv(x, y, w, k, stride, pad, scale, bias, act="none", res=None):
 
 def maxpool(x, y, k, stride, pad):
     check(lib().prpe_maxpool(C.byref(view(x)), C.byref(view(y)), k, stride, pad, _stream()), "prpe_maxpool")
+    return y
+
+
+def copy_pad(x, y):
+    check(lib().prpe_copy_pad(C.byref(view(x)), C.byref(view(y)), _stream()), "prpe_copy_pad")
     return y
 
 

@@ -206,7 +206,8 @@ def test_conv_fp32_faithful_stem_scalar_path():
 
 @pytest.mark.parametrize("hi,wi,ho,wo,ac,act", [(20, 20, 160, 160, True, "silu"), (20, 20, 112, 112, True, "prelu"),
                                                (20, 20, 256, 192, True, "gelu"), (16, 12, 64, 48, False, "none")])
-def test_upconv_equals_upsample_then_conv(hi, wi, ho, wo, ac, act):
+@pytest.mark.parametrize("separable", [True, False])
+def test_upconv_equals_upsample_then_conv(hi, wi, ho, wo, ac, act, separable):
     Ci, Co = 32, 24
     x = rnd(2, Ci, hi, wi, seed=23)
     w = rnd(Co, Ci, 3, 3, seed=24, scale=0.05)
@@ -218,7 +219,8 @@ def test_upconv_equals_upsample_then_conv(hi, wi, ho, wo, ac, act):
     z = torch.empty(2, hi, wi, 9 * Co, device=DEV)
     ops.conv2d(xd, taps, z)
     y = torch.empty(2, ho, wo, Co, device=DEV)
-    ops.upconv3x3(z, y, ac, sc.to(DEV), bi.to(DEV), sl.to(DEV) if act == "prelu" else None, act)
+    ops.upconv3x3(z, y, ac, sc.to(DEV), bi.to(DEV), sl.to(DEV) if act == "prelu" else None, act,
+                  separable=separable)
     torch.cuda.synchronize()
     u = F.interpolate(x.double(), size=(ho, wo), mode="bilinear", align_corners=ac)
     ref = F.conv2d(u, w.double(), None, 1, 1) * sc.double().view(1, -1, 1, 1) + bi.double().view(1, -1, 1, 1)

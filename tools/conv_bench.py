@@ -1,0 +1,72 @@
+"""Micro-benchmark of prpe_conv2d on the model's heaviest conv shapes (GPU box).
+
+    python tools/conv_bench.py [--batch 32] [--only NAME] [--prec 0,2] [--tiles 0]
+
+Prints per (shape, precision, tile): mean ms, algorithmic TF/s, executed TF/s (x MFMA passes).
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "person-recognition-for-pose-estimation_amd")]
+
+import torch  # noqa: E402
+
+from prpe import ops, pack  # noqa: E402
+
+# name: (H, W, Ci, Co, k, stride, pad, frames-per-batch multiplier)
+SHAPES = {
+    "vit_adapter.7 3x3 256->128 @256x192": (256, 192, 256, 128, 3, 1, 1),
+    "yolo_adapter.7 1x1 512->256 @160": (160, 160, 512, 256, 1, 1, 0),
+    "yolo_adapter.10 3x3 256->128 @160": (160, 160, 256, 128, 3, 1, 1),
+    "trunk l1 3x3 64->64 @160": (160, 160, 64, 64, 3, 1, 1),
+    "trunk l1 1x1 64->256 @160": (160, 160, 64, 256, 1, 1, 0),
+    "trunk l1 1x1 256->64 @160": (160, 160, 256, 64, 1, 1, 0),
+    "trunk l3 3x3 256->256 @40": (40, 40, 256, 256, 3, 1, 1),
+    "trunk l3 1x1 1024->256 @40": (40, 40, 1024, 256, 1, 1, 0),
+    "vit fc1 768->3072 (192 tok)": (16, 12, 768, 3072, 1, 1, 0),
+    "vit fc2 3072->768 (192 tok)": (16, 12, 3072, 768, 1, 1, 0),
+    "ada_adapter.7 3x3 256->128 @112": (112, 112, 256, 128, 3, 1, 1),
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--only", default="")
+    ap.add_argument("--prec", default="0,2")
+    ap.add_argument("--tiles", default="0")
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    dev = "cuda"
+    torch.manual_seed(0)
+    for name, (H, W, Ci, Co, k, s, p) in SHAPES.items():
+        if a.only and a.only not in name:
+            continue
+        B = a.batch
+        x = torch.rand(B, H, W, Ci, device=dev) * 2 - 1
+        w = (torch.rand(Co, Ci, k, k) * 2 - 1) / (Ci * k * k) ** 0.5
+        pk = pack.pack_conv("b", w, s, p, dev, scale=torch.ones(Co), bias=torch.zeros(Co), act="relu")
+        Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+        y = torch.empty(B, Ho, Wo, Co, device=dev)
+        fl = 2.0 * B * Ho * Wo * Co * Ci * k * k
+        for prec in [int(v) for v in a.prec.split(",")]:
+            for tile in [int(v) for v in a.tiles.split(",")]:
+                ops.conv2d(x, pk, y, precision=prec, tile=tile)
+                torch.cuda.synchronize()
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    ops.conv2d(x, pk, y, precision=prec, tile=tile)
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / a.iters
+                passes = {0: 3, 1: 1, 2: 6}[prec]
+                tf = fl / ms / 1e9
+                print(f"{name:40s} prec={prec} tile={tile} {ms:8.3f} ms  alg {tf:7.1f} TF/s  exec {tf * passes:7.1f} TF/s",
+                      flush=True)
+
+
+if __name__ == "__main__":
+    main()
