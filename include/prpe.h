@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PRPE_ABI_VERSION 1
+#define PRPE_ABI_VERSION 2
 
 /* activations (epilogues/prologues) */
 enum prpe_act {
@@ -58,8 +58,11 @@ typedef struct prpe_view {
  *   y[n,oh,ow,co] = EPI( sum_{kh,kw,ci} PRO(x[n, oh*s-p+kh, ow*s-p+kw, ci]) * W[co,kh,kw,ci] )
  * PRO(v) = v*in_scale[ci] + in_bias[ci] for in-bounds taps, 0 for padding (IR-50 pre-BN,
  * libs/net_adaface.py:159). EPI = folded BN / bias (scale, bias), residual, activation.
- * Weights are packed by the host: bf16 planes [co_pad][k_pad], k = (kh*KW+kw)*Ci+ci,
- * w = plane0 + plane1 + plane2 (RNE splits).
+ * Weights are packed by the host: bf16 planes [co_pad][k_pad], w = plane0 + plane1 + plane2
+ * (RNE splits), with k in the order ``k_order`` names:
+ *   0: k = (kh*KW+kw)*Ci + ci                          (any Ci)
+ *   1: k = ((ci/32)*KH*KW + kh*KW+kw)*32 + ci%32       (Ci % 32 == 0, channel-contiguous x:
+ *      the taps of one 32-channel chunk are consecutive K-steps -> input re-reads hit L1)
  * Replaces: torch.nn.Conv2d + BatchNorm2d (+act, +residual) in training/modify_models.py,
  * yolopt/nets/nn.py:28-39, libs/net_adaface.py:144-167, torchvision resnet50 (:446),
  * nn.Linear in ViTPose and IR-50 output_layer (as a 1x1 / 7x7 "conv").
@@ -72,7 +75,7 @@ typedef struct prpe_conv_desc {
   const uint16_t* w_hi;   /* bf16 bits, plane 0 */
   const uint16_t* w_lo;   /* plane 1 (precision 0, 2) */
   const uint16_t* w_lo2;  /* plane 2 (precision 2) */
-  int32_t k_pad, co_pad;  /* packed extents (k_pad % 32 == 0, co_pad % 64 == 0) */
+  int32_t k_pad, co_pad;  /* packed extents (k_pad % 32 == 0, co_pad % 128 == 0) */
   const float* scale;     /* [Co] or NULL (= 1) */
   const float* bias;      /* [Co] or NULL (= 0) */
   const float* slope;     /* [Co] PReLU slopes or NULL */
@@ -83,7 +86,8 @@ typedef struct prpe_conv_desc {
   int32_t precision;      /* 0 = 2-plane split-bf16, 3 MFMA terms (~2^-17);
                              2 = 3-plane split (exact fp32 operands), 6 terms;
                              1 = plain bf16 (1 term; diagnostics only) */
-  int32_t tile;           /* 0 = auto */
+  int32_t tile;           /* 0 = auto; 1..6 = 128x128, 128x64, 128x32, 128x16, 256x128, 256x64 */
+  int32_t k_order;        /* weight K order, see above */
 } prpe_conv_desc;
 
 int prpe_conv2d(const prpe_conv_desc* d, void* stream);

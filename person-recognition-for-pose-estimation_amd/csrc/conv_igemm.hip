@@ -1,8 +1,12 @@
-// Implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), split-bf16 x3.
+// Implicit-GEMM convolution on CDNA4 MFMA (v_mfma_f32_16x16x32_bf16), split-bf16 operands.
 //
-// GEMM view: M = N*Ho*Wo output pixels, N_gemm = Co, K = KH*KW*Ci (k = (kh*KW+kw)*Ci+ci).
+// GEMM view: M = N*Ho*Wo output pixels, N_gemm = Co, K = KH*KW*Ci.
 //   A[m,k] = PRO(x[n, oh*s-p+kh, ow*s-p+kw, ci])   (gathered on the fly, strided view)
-//   B[k,co] = W[co, kh, kw, ci]                    (host-packed bf16 hi/lo planes [co][k])
+//   B[k,co] = W[co, kh, kw, ci]                    (host-packed bf16 planes [co][k])
+// K order (``k_order``): 0 = tap-major k = (kh*KW+kw)*Ci + ci; 1 = chunk-major
+// k = ((ci/32)*KH*KW + kh*KW+kw)*32 + ci%32 (Ci % 32 == 0): the KH*KW taps of one 32-channel
+// chunk are consecutive K-steps, so the overlapping input windows they gather are re-read
+// from L1 instead of L2.
 // Each fp32 operand is split into NP bf16 planes a = a0 + a1 (+ a2) and the wave issues the
 // partial products with plane-index sum < NP, smallest first, fp32 accumulate:
 //   precision 0 (NP=2): a1*b0 + a0*b1 + a0*b0            ~16-bit operands, 2^-17 rel/product,
@@ -12,12 +16,14 @@
 //                        at 1/6 of the bf16 rate (~415 TF/s ceiling vs 157 for f32 MFMA)
 //   precision 1 (NP=1): a0*b0 plain bf16 (diagnostics / ablation only)
 //
-// Tiling: BM x BN x 32, 256 threads = 4 waves (WM x WN), each wave a (BM/WM)x(BN/WN) tile of
-// 16x16 MFMA blocks. Global->register prefetch of tile k+1 overlaps the MFMAs of tile k;
-// LDS double buffer, one barrier per K-step. LDS rows are 64 B (32 bf16); the 4 16-B slots
-// of row r are XOR-permuted by F[(r>>2)&3] = {0,2,3,1}, which makes every ds_read_b128
-// lane group of the fragment read hit 16 distinct slots (conflict-free).
-// Grid: 1-D, XCD-remapped so the Co-tiles sharing one A panel run on one XCD (shared L2).
+// Tiling: BM x BN x 32, NT = 64*WM*WN threads, each wave a (BM/WM)x(BN/WN) tile of 16x16 MFMA
+// blocks. Global->register prefetch of tile k+1 overlaps the MFMAs of tile k (A is split into
+// planes in registers, then written to LDS); LDS double buffer, one barrier per K-step. LDS
+// rows are 64 B (32 bf16); the 4 16-B slots of row r are XOR-permuted by F[(r>>2)&3] =
+// {0,2,3,1}, which makes every ds_read_b128 lane group of the fragment read hit 16 distinct
+// slots. Epilogue: the accumulator tile is staged through the (then free) LDS ring and written
+// as whole-row 16-B vectors with coalesced residual loads. Grid: 1-D, XCD-remapped so the
+// Co-tiles sharing one A panel run on one XCD (shared L2).
 //
 // Reference arithmetic replaced: torch Conv2d (+BatchNorm2d eval +act +residual) at every
 // call site listed in include/prpe.h (prpe_conv2d).
@@ -26,7 +32,6 @@
 namespace {
 
 constexpr int BK = 32;
-constexpr int NTHREADS = 256;
 
 struct ConvK {
   const float* x; int64_t xsn, xsh, xsw, xsc; int Hi, Wi, Ci;
@@ -48,23 +53,31 @@ __device__ __forceinline__ int swzF(int row) { return (0x78 >> (((row >> 2) & 3)
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 
-template <int BM, int BN, int WM, int WN, bool VEC, int PREC>
-__global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
+// KM: 0 = scalar gather through a k -> (kh,kw,ci) LUT (any Ci, e.g. 3-channel inputs)
+//     1 = vector loads, tap-major K (Ci % 4 == 0)
+//     2 = vector loads, chunk-major K (Ci % 32 == 0, weights packed with k_order 1)
+template <int BM, int BN, int WM, int WN, int KM, int PREC>
+__global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr bool VEC = KM != 0;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int A_ROWS_PT = BM / 32;                 // VEC: rows per thread (8 float4 per row)
+  constexpr int RPASS = NT / 8;                      // VEC: rows per pass (8 float4 per row)
+  constexpr int A_ROWS_PT = BM / RPASS;
   constexpr int B_CHUNKS = BN * 4;                   // 16-B chunks per plane per K-step
-  constexpr int B_PT = (B_CHUNKS + NTHREADS - 1) / NTHREADS;
-  static_assert(WM * WN == 4, "4 waves");
+  constexpr int B_PT = (B_CHUNKS + NT - 1) / NT;
   constexpr int NP = PREC == 1 ? 1 : (PREC == 0 ? 2 : 3);   // bf16 planes per operand
-  static_assert(TM >= 1 && TN >= 1, "tile");
+  static_assert(TM >= 1 && TN >= 1 && A_ROWS_PT >= 1, "tile");
+  static_assert(KM != 0 || (NT % BM == 0), "scalar path: NT multiple of BM");
 
-  // LDS: [buf][plane][rows][32] bf16 (u16), A then B.
-  // staging ring (2 buffers x NP planes x (A|B) tiles) re-used for the epilogue's C tile
-  constexpr int LDS_U16 = (2 * NP * (BM + BN) * BK) > (BM * (BN + 4) * 2) ? (2 * NP * (BM + BN) * BK)
-                                                                          : (BM * (BN + 4) * 2);
+  // staging ring: [buf][plane][A rows | B rows][32] bf16; re-used for the epilogue's C tile
+  constexpr int LDS_U16 = 2 * NP * (BM + BN) * BK;
+  constexpr int CS = BN + 4;                          // C-tile row pitch (floats)
+  constexpr int CH_FIT = (LDS_U16 * 2) / (CS * 4);
+  constexpr int CH = CH_FIT >= BM ? BM : (CH_FIT / 16) * 16;   // C rows staged per round
+  static_assert(CH >= 16, "epilogue staging");
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
-  __shared__ int klut[VEC ? 1 : 1024];
+  __shared__ int klut[KM == 0 ? 1024 : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -78,12 +91,9 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
   auto B_at = [&](int buf, int plane) -> uint16_t* { return lds + ((buf * NP + plane) * (BM + BN) + BM) * BK; };
 
   // ---------------- A-load state
-  // VEC: thread -> k chunk c4 = tid&7 (4 floats), rows tid/8 + 32*i.
-  // scalar: thread -> row tid % BM, k columns kk0 + (256/BM)*j.
-  constexpr int S_ROWS = 1;
-  constexpr int S_KPT = (BM * BK) / NTHREADS;          // k elements per thread per step (scalar)
-  int64_t rowoff[VEC ? A_ROWS_PT : S_ROWS];
-  int ih0[VEC ? A_ROWS_PT : S_ROWS], iw0[VEC ? A_ROWS_PT : S_ROWS];
+  constexpr int S_KPT = (BM * BK) / NT;               // scalar: k elements per thread per step
+  int64_t rowoff[VEC ? A_ROWS_PT : 1];
+  int ih0[VEC ? A_ROWS_PT : 1], iw0[VEC ? A_ROWS_PT : 1];
 
   auto decode_row = [&](int m, int64_t& off, int& ih, int& iw) {
     if (m < p.M) {
@@ -101,11 +111,11 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
 
   if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < A_ROWS_PT; ++i) decode_row(m0 + (tid >> 3) + 32 * i, rowoff[i], ih0[i], iw0[i]);
+    for (int i = 0; i < A_ROWS_PT; ++i) decode_row(m0 + (tid >> 3) + RPASS * i, rowoff[i], ih0[i], iw0[i]);
   } else {
     decode_row(m0 + (tid % BM), rowoff[0], ih0[0], iw0[0]);
     // k -> packed (dh, dw, ci) table for this layer (k_pad <= 1024 checked on host)
-    for (int k = tid; k < p.k_pad; k += NTHREADS) {
+    for (int k = tid; k < p.k_pad; k += NT) {
       int v = -1;
       if (k < p.K) {
         int tap = k / p.Ci, ci = k - tap * p.Ci;
@@ -117,11 +127,12 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
     __syncthreads();
   }
 
-  // VEC incremental (kh, kw, ci) of this thread's chunk
+  // KM 1: incremental (kh, kw, ci) of this thread's chunk
   int c_ci = (tid & 7) * 4, c_kh = 0, c_kw = 0;
-  if constexpr (VEC) {
+  if constexpr (KM == 1) {
     while (c_ci >= p.Ci) { c_ci -= p.Ci; if (++c_kw == p.KW) { c_kw = 0; ++c_kh; } }
   }
+  const int khw = p.KH * p.KW;
 
   f4 areg[VEC ? A_ROWS_PT : 1];
   float sreg[VEC ? 1 : S_KPT];
@@ -129,28 +140,39 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
 
   auto load_tile = [&](int kt) {
     if constexpr (VEC) {
-      const bool kval = c_kh < p.KH;
+      int kh, kw, ci;
+      bool kval;
+      if constexpr (KM == 2) {
+        const int chunk = kt / khw, tap = kt - chunk * khw;
+        kh = tap / p.KW; kw = tap - kh * p.KW;
+        ci = chunk * BK + (tid & 7) * 4;
+        kval = true;
+      } else {
+        kh = c_kh; kw = c_kw; ci = c_ci;
+        kval = c_kh < p.KH;
+      }
       f4 s4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
       if (p.in_scale && kval) {
-        s4 = *reinterpret_cast<const f4*>(p.in_scale + c_ci);
-        b4 = *reinterpret_cast<const f4*>(p.in_bias + c_ci);
+        s4 = *reinterpret_cast<const f4*>(p.in_scale + ci);
+        b4 = *reinterpret_cast<const f4*>(p.in_bias + ci);
       }
 #pragma unroll
       for (int i = 0; i < A_ROWS_PT; ++i) {
-        const int ih = ih0[i] + c_kh, iw = iw0[i] + c_kw;
+        const int ih = ih0[i] + kh, iw = iw0[i] + kw;
         f4 v = {0.f, 0.f, 0.f, 0.f};
         if (kval && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) {
-          v = *reinterpret_cast<const f4*>(p.x + rowoff[i] + ih * p.xsh + iw * p.xsw + c_ci);
+          v = *reinterpret_cast<const f4*>(p.x + rowoff[i] + ih * p.xsh + iw * p.xsw + ci);
           if (p.in_scale) v = v * s4 + b4;
         }
         areg[i] = v;
       }
-      // advance this thread's k by BK
-      c_ci += BK;
-      while (c_ci >= p.Ci && c_kh < p.KH) { c_ci -= p.Ci; if (++c_kw == p.KW) { c_kw = 0; ++c_kh; } }
+      if constexpr (KM == 1) {
+        c_ci += BK;
+        while (c_ci >= p.Ci && c_kh < p.KH) { c_ci -= p.Ci; if (++c_kw == p.KW) { c_kw = 0; ++c_kh; } }
+      }
     } else {
       const int kk0 = tid / BM;
-      constexpr int KSTEP = NTHREADS / BM;
+      constexpr int KSTEP = NT / BM;
 #pragma unroll
       for (int j = 0; j < S_KPT; ++j) {
         const int k = kt * BK + kk0 + KSTEP * j;
@@ -170,8 +192,8 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
     // B: packed planes [co_pad][k_pad] bf16
 #pragma unroll
     for (int j = 0; j < B_PT; ++j) {
-      const int c = tid + NTHREADS * j;
-      if (B_CHUNKS % NTHREADS == 0 || c < B_CHUNKS) {
+      const int c = tid + NT * j;
+      if (B_CHUNKS % NT == 0 || c < B_CHUNKS) {
         const int row = c >> 2, ch = c & 3;
         const int64_t off = (int64_t)(n0 + row) * p.k_pad + kt * BK + ch * 8;
         breg[0][j] = *reinterpret_cast<const u4*>(p.whi + off);
@@ -186,15 +208,14 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
       const int c4 = tid & 7;
 #pragma unroll
       for (int i = 0; i < A_ROWS_PT; ++i) {
-        const int row = (tid >> 3) + 32 * i;
+        const int row = (tid >> 3) + RPASS * i;
         const int slot = (c4 >> 1) ^ swzF(row);
         const int off = row * BK + slot * 8 + (c4 & 1) * 4;
         bf16x4 pl[NP];
         const f4 v = areg[i];
-        const float vv[4] = {v[0], v[1], v[2], v[3]};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          float r = vv[e];
+          float r = v[e];
 #pragma unroll
           for (int q = 0; q < NP; ++q) {
             const __bf16 t = (__bf16)r;
@@ -207,7 +228,7 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
       }
     } else {
       const int row = tid % BM, kk0 = tid / BM;
-      constexpr int KSTEP = NTHREADS / BM;
+      constexpr int KSTEP = NT / BM;
 #pragma unroll
       for (int j = 0; j < S_KPT; ++j) {
         const int kk = kk0 + KSTEP * j;
@@ -224,8 +245,8 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
     }
 #pragma unroll
     for (int j = 0; j < B_PT; ++j) {
-      const int c = tid + NTHREADS * j;
-      if (B_CHUNKS % NTHREADS == 0 || c < B_CHUNKS) {
+      const int c = tid + NT * j;
+      if (B_CHUNKS % NT == 0 || c < B_CHUNKS) {
         const int row = c >> 2, ch = c & 3;
         const int off = row * BK + (ch ^ swzF(row)) * 8;
 #pragma unroll
@@ -259,7 +280,6 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
       for (int q = 0; q < NP; ++q) bfr[q][j] = *reinterpret_cast<const bf16x8*>(B_at(buf, q) + off);
     }
     // partial products smallest first; terms with plane-index sum >= NP are dropped
-    // (NP=2: lo*hi + hi*lo + hi*hi; NP=3: 2*0 + 1*1 + 0*2 + 1*0 + 0*1 + 0*0)
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -286,46 +306,53 @@ __global__ __launch_bounds__(NTHREADS) void conv_igemm_kernel(ConvK p) {
 
   // ---------------- epilogue
   if (p.vec_out) {
-    // Stage the raw accumulator tile through LDS (free after the loop's last barrier), then
-    // every thread owns 16-B column chunks of whole rows: coalesced float4 residual loads and
-    // output stores (a wave moves 1 KB per instruction) instead of 64-B row fragments.
-    constexpr int CS = BN + 4;                      // padded row (floats)
+    // Stage the raw accumulator tile through LDS (CH rows per round), then every thread owns
+    // 16-B column chunks of whole rows: coalesced float4 residual loads and output stores.
     float* ct = reinterpret_cast<float*>(lds);
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          ct[(wm * WTM + i * 16 + fg * 4 + r) * CS + wn * WTN + j * 16 + fr] = acc[i][j][r];
-    __syncthreads();
     constexpr int CPR = BN / 4;                     // float4 chunks per tile row
-    constexpr int RPP = NTHREADS / CPR;             // rows per pass
+    constexpr int RPP = NT / CPR;                   // rows per pass
     const int cc = tid % CPR;
     const int col = n0 + cc * 4;
+    f4 sc4 = {1.f, 1.f, 1.f, 1.f}, bi4 = {0.f, 0.f, 0.f, 0.f}, sl4 = {0.f, 0.f, 0.f, 0.f};
     if (col < p.Co) {
-      f4 sc4 = {1.f, 1.f, 1.f, 1.f}, bi4 = {0.f, 0.f, 0.f, 0.f}, sl4 = {0.f, 0.f, 0.f, 0.f};
       if (p.scale) sc4 = *reinterpret_cast<const f4*>(p.scale + col);
       if (p.bias) bi4 = *reinterpret_cast<const f4*>(p.bias + col);
       if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
-      for (int rr = tid / CPR; rr < BM; rr += RPP) {
-        const int m = m0 + rr;
-        if (m >= p.M) break;
-        const int n = m / p.HoWo;
-        const int rem = m - n * p.HoWo;
-        const int oh = rem / p.Wo;
-        const int ow = rem - oh * p.Wo;
-        f4 v = *reinterpret_cast<const f4*>(ct + rr * CS + cc * 4);
-        v = v * sc4 + bi4;
-        f4 res = {0.f, 0.f, 0.f, 0.f};
-        if (p.res_mode != PRPE_RES_NONE)
-          res = *reinterpret_cast<const f4*>(p.r + (int64_t)n * p.rsn + (int64_t)oh * p.rsh + (int64_t)ow * p.rsw + col);
-        if (p.res_mode == PRPE_RES_PRE_ACT) v += res;
+    }
+    for (int h0 = 0; h0 < BM; h0 += CH) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act, sl4[e]);
-        if (p.res_mode == PRPE_RES_POST_ACT) v += res;
-        *reinterpret_cast<f4*>(p.y + (int64_t)n * p.ysn + (int64_t)oh * p.ysh + (int64_t)ow * p.ysw + col) = v;
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = wm * WTM + i * 16 + fg * 4 + r - h0;
+          if (row >= 0 && row < CH)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) ct[row * CS + wn * WTN + j * 16 + fr] = acc[i][j][r];
+        }
+      __syncthreads();
+      if (col < p.Co) {
+        const int rows = BM - h0 < CH ? BM - h0 : CH;
+        for (int rr = tid / CPR; rr < rows; rr += RPP) {
+          const int m = m0 + h0 + rr;
+          if (m >= p.M) break;
+          const int n = m / p.HoWo;
+          const int rem = m - n * p.HoWo;
+          const int oh = rem / p.Wo;
+          const int ow = rem - oh * p.Wo;
+          f4 v = *reinterpret_cast<const f4*>(ct + rr * CS + cc * 4);
+          v = v * sc4 + bi4;
+          f4 res = {0.f, 0.f, 0.f, 0.f};
+          if (p.res_mode != PRPE_RES_NONE)
+            res = *reinterpret_cast<const f4*>(p.r + (int64_t)n * p.rsn + (int64_t)oh * p.rsh +
+                                              (int64_t)ow * p.rsw + col);
+          if (p.res_mode == PRPE_RES_PRE_ACT) v += res;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act, sl4[e]);
+          if (p.res_mode == PRPE_RES_POST_ACT) v += res;
+          *reinterpret_cast<f4*>(p.y + (int64_t)n * p.ysn + (int64_t)oh * p.ysh + (int64_t)ow * p.ysw + col) = v;
+        }
       }
+      if (h0 + CH < BM) __syncthreads();
     }
     return;
   }
@@ -441,23 +468,26 @@ __global__ __launch_bounds__(256) void conv_smallco_kernel(ConvK p, int lpp_log2
   }
 }
 
+template <int BM, int BN, int WM, int WN, int KM>
+int launch_km(const ConvK& kp, int prec, dim3 grid, hipStream_t st) {
+  constexpr int NT = 64 * WM * WN;
+  if (prec == 0) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, KM, 0>), grid, dim3(NT), 0, st, kp);
+  else if (prec == 1) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, KM, 1>), grid, dim3(NT), 0, st, kp);
+  else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, KM, 2>), grid, dim3(NT), 0, st, kp);
+  return launch_status();
+}
+
 template <int BM, int BN, int WM, int WN>
-int launch_cfg(const ConvK& kp0, bool vec, int prec, hipStream_t st) {
+int launch_cfg(const ConvK& kp0, int km, int prec, hipStream_t st) {
   ConvK kp = kp0;
   const int tiles_m = (kp.M + BM - 1) / BM;
   kp.tiles_n = (kp.Co + BN - 1) / BN;
   kp.nwg = tiles_m * kp.tiles_n;
-  dim3 grid(kp.nwg), block(NTHREADS);
-  if (vec) {
-    if (prec == 0) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, true, 0>), grid, block, 0, st, kp);
-    else if (prec == 1) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, true, 1>), grid, block, 0, st, kp);
-    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, true, 2>), grid, block, 0, st, kp);
-  } else {
-    if (prec == 0) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, false, 0>), grid, block, 0, st, kp);
-    else if (prec == 1) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, false, 1>), grid, block, 0, st, kp);
-    else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, false, 2>), grid, block, 0, st, kp);
-  }
-  return launch_status();
+  dim3 grid(kp.nwg);
+  if (km == 2) return launch_km<BM, BN, WM, WN, 2>(kp, prec, grid, st);
+  if (km == 1) return launch_km<BM, BN, WM, WN, 1>(kp, prec, grid, st);
+  if constexpr ((64 * WM * WN) % BM == 0) return launch_km<BM, BN, WM, WN, 0>(kp, prec, grid, st);
+  return PRPE_EINVAL;
 }
 
 }  // namespace
@@ -478,12 +508,16 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   if (d->res_mode != PRPE_RES_NONE && !d->res.ptr) return PRPE_EINVAL;
   if (d->in_scale && !d->in_bias) return PRPE_EINVAL;
   if (d->act == PRPE_ACT_PRELU && !d->slope) return PRPE_EINVAL;
+  if (d->k_order != 0 && d->k_order != 1) return PRPE_EINVAL;
   const int64_t M64 = (int64_t)x.n * Ho * Wo;
   if (M64 >= (1LL << 31)) return PRPE_EINVAL;
   // vector path: contiguous channels, Ci % 4 == 0, 16-B aligned rows
   const bool vec = x.sc == 1 && (x.c % 4) == 0 && (x.sw % 4) == 0 && (x.sh % 4) == 0 &&
                    (x.sn % 4) == 0 && ((uintptr_t)x.ptr % 16) == 0;
-  if (!vec && d->k_pad > 1024) return PRPE_EINVAL;
+  // chunk-major K needs the vector path and whole 32-channel chunks
+  if (d->k_order == 1 && (!vec || x.c % 32 != 0)) return PRPE_EINVAL;
+  const int km = d->k_order == 1 ? 2 : (vec ? 1 : 0);
+  if (km == 0 && d->k_pad > 1024) return PRPE_EINVAL;
 
   ConvK kp{};
   kp.x = x.ptr; kp.xsn = x.sn; kp.xsh = x.sh; kp.xsw = x.sw; kp.xsc = x.sc;
@@ -508,34 +542,36 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   hipStream_t st = as_stream(stream);
   const int prec = d->precision;
   int tile = d->tile;
-  // direct fp32 kernel for tiny Co (needs the 3 weight planes; exact fp32 products)
+  // direct fp32 kernel for tiny Co (needs the 3 weight planes; exact fp32 products); 1x1 only:
+  // for 3x3 Co=3 the MFMA path measured faster (7.5 ms vs 11.8 ms at bs=256)
   const int khw = d->kh * d->kw;
-  // (3x3 Co=3 stays on the MFMA path: measured 7.5 ms vs 11.8 ms for this kernel at bs=256)
-  if (tile == 0 && y.c <= 4 && vec && !d->in_scale && d->w_lo && d->w_lo2 && x.c <= 256 && khw == 1) {
+  if (tile == 0 && y.c <= 4 && km == 1 && !d->in_scale && d->w_lo && d->w_lo2 && x.c <= 256 && khw == 1) {
     int lg = 0;
     while ((1 << lg) * 4 < x.c) ++lg;
     const int ppb = 4 * (64 >> lg);                      // pixels per block-iteration
     int blocks = (kp.M + ppb - 1) / ppb;
     if (blocks > 256 * 16) blocks = 256 * 16;
-    if (y.c == 1) {
-      if (khw == 1) hipLaunchKernelGGL((conv_smallco_kernel<1, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
-      else hipLaunchKernelGGL((conv_smallco_kernel<1, 9>), dim3(blocks), dim3(256), 0, st, kp, lg);
-    } else if (y.c <= 3) {
-      if (khw == 1) hipLaunchKernelGGL((conv_smallco_kernel<3, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
-      else hipLaunchKernelGGL((conv_smallco_kernel<3, 9>), dim3(blocks), dim3(256), 0, st, kp, lg);
-    } else {
-      if (khw == 1) hipLaunchKernelGGL((conv_smallco_kernel<4, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
-      else hipLaunchKernelGGL((conv_smallco_kernel<4, 9>), dim3(blocks), dim3(256), 0, st, kp, lg);
-    }
+    if (y.c == 1) hipLaunchKernelGGL((conv_smallco_kernel<1, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
+    else if (y.c <= 3) hipLaunchKernelGGL((conv_smallco_kernel<3, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
+    else hipLaunchKernelGGL((conv_smallco_kernel<4, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
     return launch_status();
   }
-  // measured (tools/conv_bench.py): 3-plane mode prefers 128x64 (LDS 72 KB -> 2 blocks/CU)
-  if (tile == 0) tile = (y.c > 64 && prec != 2) ? 1 : y.c > 32 ? 2 : y.c > 16 ? 3 : 4;
+  // measured (tools/conv_bench.py, profiles/r01_conv_bench_tiles.txt): the 3-plane mode wants the
+  // 256x128 8-wave tile for wide Co (operand traffic per MFMA halves; +30%), 128x64 below;
+  // the 2-plane mode is near-flat between 128x128 and 256x128 (256x128 +2% on 3x3) and
+  // prefers 256x64 for Co <= 64
+  if (tile == 0) {
+    if (y.c > 64) tile = (prec == 2 || khw > 1) ? 5 : 1;
+    else if (y.c > 32) tile = prec == 2 ? 2 : 6;
+    else tile = y.c > 16 ? 3 : 4;
+  }
   switch (tile) {
-    case 1: return launch_cfg<128, 128, 2, 2>(kp, vec, prec, st);
-    case 2: return launch_cfg<128, 64, 2, 2>(kp, vec, prec, st);
-    case 3: return launch_cfg<128, 32, 4, 1>(kp, vec, prec, st);
-    case 4: return launch_cfg<128, 16, 4, 1>(kp, vec, prec, st);
+    case 1: return launch_cfg<128, 128, 2, 2>(kp, km, prec, st);
+    case 2: return launch_cfg<128, 64, 2, 2>(kp, km, prec, st);
+    case 3: return launch_cfg<128, 32, 4, 1>(kp, km, prec, st);
+    case 4: return launch_cfg<128, 16, 4, 1>(kp, km, prec, st);
+    case 5: return launch_cfg<256, 128, 4, 2>(kp, km, prec, st);
+    case 6: return launch_cfg<256, 64, 4, 2>(kp, km, prec, st);
     default: return PRPE_EINVAL;
   }
 }

@@ -11,7 +11,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libprpe.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 
 class PrpeError(RuntimeError):
@@ -31,7 +31,8 @@ class ConvDesc(C.Structure):
                 ("k_pad", C.c_int32), ("co_pad", C.c_int32),
                 ("scale", C.c_void_p), ("bias", C.c_void_p), ("slope", C.c_void_p),
                 ("in_scale", C.c_void_p), ("in_bias", C.c_void_p),
-                ("act", C.c_int32), ("res_mode", C.c_int32), ("precision", C.c_int32), ("tile", C.c_int32)]
+                ("act", C.c_int32), ("res_mode", C.c_int32), ("precision", C.c_int32), ("tile", C.c_int32),
+                ("k_order", C.c_int32)]
 
 
 ACT = {"none": 0, "relu": 1, "silu": 2, "prelu": 3, "gelu": 4, "sigmoid": 5}

@@ -51,6 +51,7 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
     d.res_mode = res_mode
     d.precision = precision
     d.tile = tile
+    d.k_order = pack.k_order
     check(lib().prpe_conv2d(C.byref(d), _stream()), f"prpe_conv2d[{pack.name}]")
     return y
 

@@ -2,8 +2,10 @@
 
 A ``ConvPack`` holds the weight of one conv / linear in the layout the implicit-GEMM
 kernel streams (include/prpe.h, prpe_conv2d):
-  * W[co, ci, kh, kw] -> [co][(kh*KW + kw)*Ci + ci], zero-padded to [co_pad][k_pad]
-    (k_pad % 32 == 0, co_pad % 128 == 0), split into three bf16 planes
+  * W[co, ci, kh, kw] -> [co][k], zero-padded to [co_pad][k_pad] (k_pad % 32 == 0,
+    co_pad % 128 == 0), with k tap-major (k_order 0: k = (kh*KW + kw)*Ci + ci) or, for
+    KH*KW > 1 and Ci % 32 == 0, chunk-major (k_order 1: k = ((ci/32)*KH*KW + kh*KW+kw)*32
+    + ci%32, the 9 taps of one 32-channel chunk adjacent), split into three bf16 planes
     (p0 = RNE(w), p1 = RNE(w - p0), p2 = RNE(w - p0 - p1); p0+p1+p2 == w exactly);
   * the epilogue's per-channel affine: eval BatchNorm folded exactly as PyTorch's CPU
     batch_norm inference does (alpha = gamma / sqrt(var + eps), beta' = beta - mean*alpha),
@@ -42,6 +44,7 @@ class ConvPack:
     in_scale: torch.Tensor | None = None
     in_bias: torch.Tensor | None = None
     act: str = "none"
+    k_order: int = 0
 
     @property
     def flops_per_pixel(self) -> int:
@@ -75,8 +78,8 @@ def bn_affine(sd, prefix, eps, conv_bias=None):
 
 
 def pack_matrix(name, w2d: torch.Tensor, kh, kw, ci, stride, pad, device, scale=None, bias=None,
-                slope=None, in_scale=None, in_bias=None, act="none") -> ConvPack:
-    """w2d: [co, K] with K ordered (kh, kw, ci)."""
+                slope=None, in_scale=None, in_bias=None, act="none", k_order=0) -> ConvPack:
+    """w2d: [co, K] with K in the order ``k_order`` names (see module docstring)."""
     co, K = w2d.shape
     k_pad, co_pad = _rup(K, 32), _rup(co, 128)
     wp = torch.zeros(co_pad, k_pad, dtype=torch.float32)
@@ -85,14 +88,21 @@ def pack_matrix(name, w2d: torch.Tensor, kh, kw, ci, stride, pad, device, scale=
     dev = lambda t: None if t is None else t.float().contiguous().to(device)
     return ConvPack(name, p0.contiguous().to(device), p1.contiguous().to(device), p2.contiguous().to(device), kh, kw,
                     stride, pad, ci, co, k_pad, co_pad, dev(scale), dev(bias), dev(slope), dev(in_scale),
-                    dev(in_bias), act)
+                    dev(in_bias), act, k_order)
 
 
-def pack_conv(name, w: torch.Tensor, stride=1, pad=0, device="cuda", **kw) -> ConvPack:
-    """w: [co, ci, kh, kw] (PyTorch layout)."""
+def pack_conv(name, w: torch.Tensor, stride=1, pad=0, device="cuda", k_order="auto", **kw) -> ConvPack:
+    """w: [co, ci, kh, kw] (PyTorch layout). k_order "auto" picks chunk-major whenever it
+    applies (KH*KW > 1, Ci % 32 == 0); the input view must then be channel-contiguous."""
     co, ci, kh, kw_ = w.shape
-    w2d = w.float().permute(0, 2, 3, 1).reshape(co, kh * kw_ * ci)
-    return pack_matrix(name, w2d, kh, kw_, ci, stride, pad, device, **kw)
+    if k_order == "auto":
+        k_order = 1 if kh * kw_ > 1 and ci % 32 == 0 else 0
+    if k_order == 1:
+        assert ci % 32 == 0, name
+        w2d = w.float().reshape(co, ci // 32, 32, kh, kw_).permute(0, 1, 3, 4, 2).reshape(co, -1)
+    else:
+        w2d = w.float().permute(0, 2, 3, 1).reshape(co, kh * kw_ * ci)
+    return pack_matrix(name, w2d, kh, kw_, ci, stride, pad, device, k_order=k_order, **kw)
 
 
 def pack_upconv_taps(name, w: torch.Tensor, device="cuda") -> ConvPack:

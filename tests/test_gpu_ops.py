@@ -12,7 +12,7 @@ import torch
 import torch.nn.functional as F
 
 from prpe import ops, pack
-from prpe._lib import RES_POST, RES_PRE
+from prpe._lib import RES_POST, RES_PRE, PrpeError
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
@@ -42,10 +42,10 @@ def act_ref(v, act, slope=None):
 
 
 def run_conv(x_nchw, w, stride, pad, act="none", scale=None, bias=None, slope=None, in_s=None, in_b=None,
-             res=None, res_mode=0, precision=0, tile=0, x_layout="nhwc"):
+             res=None, res_mode=0, precision=0, tile=0, x_layout="nhwc", k_order="auto"):
     co = w.shape[0]
     p = pack.pack_conv("t", w, stride, pad, DEV, scale=scale, bias=bias, slope=slope, in_scale=in_s,
-                       in_bias=in_b, act=act)
+                       in_bias=in_b, act=act, k_order=k_order)
     if x_layout == "nchw":
         xd = ops.nhwc(x_nchw.to(DEV))
     else:
@@ -148,13 +148,60 @@ def test_conv_prologue_affine_zero_padding():
     torch.testing.assert_close(got, ref, rtol=0, atol=2e-4)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4])
-def test_conv_every_tile_config(tile):
+@pytest.mark.parametrize("k_order", [0, 1])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
+def test_conv_every_tile_config(tile, k_order):
     x = rnd(2, 64, 9, 13, seed=17)
     w = rnd(150, 64, 3, 3, seed=18, scale=0.05)
-    got = run_conv(x, w, 1, 1, tile=tile)
+    got = run_conv(x, w, 1, 1, tile=tile, k_order=k_order)
     ref = ref_conv(x, w, 1, 1)
     torch.testing.assert_close(got, ref, rtol=0, atol=2e-4)
+
+
+@pytest.mark.parametrize("precision", [0, 1, 2])
+@pytest.mark.parametrize("tile", [5, 6])
+def test_conv_256_row_tiles_chunked_epilogue(tile, precision):
+    """256-row tiles stage the C tile through LDS in row chunks (fewer rows fit when the ring
+    holds fewer planes); residual + PReLU exercise the vector epilogue across chunk borders."""
+    x = rnd(3, 96, 13, 17, seed=60)
+    w = rnd(136, 96, 3, 3, seed=61, scale=0.03)
+    r = rnd(3, 136, 13, 17, seed=62)
+    sc = torch.rand(136, generator=_g(63)) + 0.5
+    bi = rnd(136, seed=64)
+    sl = torch.rand(136, generator=_g(65)) * 0.4
+    got = run_conv(x, w, 1, 1, act="prelu", scale=sc, bias=bi, slope=sl, res=r, res_mode=RES_PRE,
+                   precision=precision, tile=tile)
+    ref = ref_conv(x, w, 1, 1, act="prelu", scale=sc, bias=bi, slope=sl, res=r, res_mode=RES_PRE)
+    torch.testing.assert_close(got, ref, rtol=0, atol=2e-2 if precision == 1 else 2e-4)
+
+
+@pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", [
+    (2, 64, 17, 19, 96, 3, 1, 1),
+    (2, 128, 11, 9, 64, 3, 2, 1),
+    (1, 512, 7, 7, 64, 7, 1, 0),
+    (2, 32, 10, 10, 40, 5, 1, 2),
+])
+def test_conv_chunk_major_matches_tap_major(B, Ci, H, W, Co, k, s, p):
+    """k_order 1 (chunk-major K) is a pure re-ordering of the reduction: same result as
+    tap-major within rounding, for 3x3/5x5/7x7 and strided convs, with the IR-50 prologue."""
+    x = rnd(B, Ci, H, W, seed=66)
+    w = rnd(Co, Ci, k, k, seed=67, scale=1.0 / math.sqrt(Ci * k * k))
+    s_in = torch.rand(Ci, generator=_g(68)) + 0.5
+    b_in = rnd(Ci, seed=69)
+    ref = ref_conv(x, w, s, p, in_s=s_in, in_b=b_in)
+    for ko in (0, 1):
+        got = run_conv(x, w, s, p, in_s=s_in, in_b=b_in, k_order=ko, precision=2)
+        torch.testing.assert_close(got, ref, rtol=0, atol=1e-5)
+
+
+def test_conv_chunk_major_rejects_unaligned_input():
+    """k_order 1 needs channel-contiguous 16-B aligned rows: a channel-offset view fails loudly."""
+    big = rnd(1, 6, 6, 66, seed=70).to(DEV)
+    xin = big[..., 2:66]                        # 64 channels at an 8-B offset
+    w = rnd(8, 64, 3, 3, seed=71)
+    p = pack.pack_conv("t", w, 1, 1, DEV, k_order=1)
+    with pytest.raises(PrpeError):
+        ops.conv2d(xin, p, torch.empty(1, 6, 6, 8, device=DEV))
 
 
 def test_conv_strided_views_in_and_out():
@@ -187,7 +234,7 @@ def test_conv_precision_modes_ordering():
     assert e6 <= 10 * f32 + 1e-6, (e6, f32)
 
 
-@pytest.mark.parametrize("tile", [1, 2, 3, 4])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6])
 def test_conv_fp32_faithful_mode_every_tile(tile):
     x = rnd(2, 64, 9, 13, seed=46)
     w = rnd(150, 64, 3, 3, seed=47, scale=0.05)

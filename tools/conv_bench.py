@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--prec", default="0,2")
     ap.add_argument("--tiles", default="0")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--korders", default="0,1", help="weight K orders to compare (1 = chunk-major)")
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -47,11 +48,17 @@ def main():
         B = a.batch
         x = torch.rand(B, H, W, Ci, device=dev) * 2 - 1
         w = (torch.rand(Co, Ci, k, k) * 2 - 1) / (Ci * k * k) ** 0.5
-        pk = pack.pack_conv("b", w, s, p, dev, scale=torch.ones(Co), bias=torch.zeros(Co), act="relu")
+        pks = {}
+        for ko in [int(v) for v in a.korders.split(",")]:
+            if ko == 1 and (k == 1 or Ci % 32):
+                continue
+            pks[ko] = pack.pack_conv("b", w, s, p, dev, scale=torch.ones(Co), bias=torch.zeros(Co), act="relu",
+                                     k_order=ko)
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         y = torch.empty(B, Ho, Wo, Co, device=dev)
         fl = 2.0 * B * Ho * Wo * Co * Ci * k * k
-        for prec in [int(v) for v in a.prec.split(",")]:
+        for (ko, pk) in pks.items():
+          for prec in [int(v) for v in a.prec.split(",")]:
             for tile in [int(v) for v in a.tiles.split(",")]:
                 ops.conv2d(x, pk, y, precision=prec, tile=tile)
                 torch.cuda.synchronize()
@@ -64,7 +71,7 @@ def main():
                 ms = e0.elapsed_time(e1) / a.iters
                 passes = {0: 3, 1: 1, 2: 6}[prec]
                 tf = fl / ms / 1e9
-                print(f"{name:40s} prec={prec} tile={tile} {ms:8.3f} ms  alg {tf:7.1f} TF/s  exec {tf * passes:7.1f} TF/s",
+                print(f"{name:40s} ko={ko} prec={prec} tile={tile} {ms:8.3f} ms  alg {tf:7.1f} TF/s  exec {tf * passes:7.1f} TF/s",
                       flush=True)
 
 
