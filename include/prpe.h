@@ -100,9 +100,10 @@ int prpe_conv2d(const prpe_conv_desc* d, void* stream);
  * align_corners = 1: src = dst*(in-1)/(out-1);  0: src = max(0,(dst+0.5)*in/out-0.5).
  * Replaces nn.Upsample(bilinear) + Conv2d(3x3) + BN + act in modify_models.py:47-52,
  * :237-242, :359-364 and the ViTPose simple decoder (modeling_vitpose.py:120-144).
- * With a workspace of >= prpe_upconv3x3_workspace_bytes(z, y) bytes the sum is evaluated
- * separably (x-interpolation into the workspace, then y; 6 loads per output instead of
- * 36); workspace = NULL selects the direct one-pass kernel.
+ * workspace = NULL (the product path) selects the fused one-pass kernel: x-interpolated
+ * source rows are kept in rolling registers, HBM traffic = y write + z read. With a workspace
+ * of >= prpe_upconv3x3_workspace_bytes(z, y) bytes the sum is instead evaluated in two passes
+ * through it (x-interpolation, then y; kept for ablation). Both give identical results.
  */
 int64_t prpe_upconv3x3_workspace_bytes(const prpe_view* z, const prpe_view* y);
 int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,

@@ -1,5 +1,6 @@
 // Memory-bound kernels of the hot path (HBM / L2 bound, VALU, wave64).
-//   upconv3x3     : bilinear-upsample o conv3x3 rewrite, stage 2 (interp of per-tap GEMMs)
+//   upconv3x3     : bilinear-upsample o conv3x3 rewrite, stage 2 (interp of per-tap GEMMs;
+//                   fused rolling-row kernel, or separable through a workspace)
 //   dwconv        : depthwise kxk conv + folded BN + act (+ residual)
 //   maxpool       : kxk/s/p max pooling
 //   upsample2x    : nearest x2
@@ -33,78 +34,117 @@ __device__ __forceinline__ void bilin_src(int dst, int in, int out, int ac, int&
   l1 = src - (float)i0;
 }
 
+// Launch geometry of the row kernels below: a 1-D grid of rows x chunks blocks, block b ->
+// row = b / chunks (one output row (n, oy), decoded once per block on the scalar unit) and
+// position (b % chunks) * 256 + threadIdx.x inside the row (pixel-major, channel group
+// fastest). All chunks of a row are adjacent in dispatch order, so the blocks in flight cover
+// a few consecutive rows (shared interpolation sources stay in L2). Per-thread index math is
+// 32-bit.
+__device__ __forceinline__ void row_pos(int chunks, int& row, int& j) {
+  row = blockIdx.x / chunks;
+  j = (blockIdx.x - row * chunks) * 256 + threadIdx.x;
+}
 struct UpK {
   prpe_view z, y;
   int Co, ac;
   const float* scale; const float* bias; const float* slope; int act;
-  int64_t total;  // N*Ho*Wo*(Co/VW)
+  int per_row;    // Wo * (Co / VW)
+  int chunks;     // ceil(per_row / 256)
 };
 
-// One thread = VW consecutive output channels of one output pixel.
+// Fused one-pass form (no workspace). One thread = VW channels of one output column, for a
+// range of R consecutive output rows (block = 256 columns x one row range, the row range is
+// block-uniform so the vertical source rows/weights live in SGPRs). The x-interpolated
+// rows H_dy[r] = sum_dx valid * lerp_x(Z_{dy,dx}[r], sx(ox+dx-1)) are kept in two rolling
+// registers per dy (rows y0 and y0+1 of the current source interval): moving down one output
+// row advances the interval by at most one source row when upsampling, so each H row is built
+// once per thread (6 L2 loads) instead of once per output row. HBM traffic is the output
+// write plus the small z read. Same arithmetic, same order as the separable form.
 template <int VW>
-__global__ __launch_bounds__(256) void upconv3x3_kernel(UpK p) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= p.total) return;
-  const int cgroups = p.Co / VW;
-  const int cg = (int)(t % cgroups);
-  int64_t pix = t / cgroups;
-  const int Ho = p.y.h, Wo = p.y.w, Hi = p.z.h, Wi = p.z.w;
-  const int ox = (int)(pix % Wo); pix /= Wo;
-  const int oy = (int)(pix % Ho);
-  const int n = (int)(pix / Ho);
-  const int c0 = cg * VW;
-  float acc[VW];
+__device__ __forceinline__ void up_hrow(const UpK& p, int n, int r, int dy, int ox, int c0,
+                                       float (&h)[VW]) {
+  const int Wo = p.y.w, Wi = p.z.w;
 #pragma unroll
-  for (int v = 0; v < VW; ++v) acc[v] = 0.f;
+  for (int v = 0; v < VW; ++v) h[v] = 0.f;
 #pragma unroll
-  for (int dy = 0; dy < 3; ++dy) {
-    const int yy = oy + dy - 1;
-    if ((unsigned)yy >= (unsigned)Ho) continue;
-    int y0, y1; float ly;
-    bilin_src(yy, Hi, Ho, p.ac, y0, y1, ly);
-#pragma unroll
-    for (int dx = 0; dx < 3; ++dx) {
-      const int xx = ox + dx - 1;
-      if ((unsigned)xx >= (unsigned)Wo) continue;
-      int x0, x1; float lx;
-      bilin_src(xx, Wi, Wo, p.ac, x0, x1, lx);
-      const int tap = dy * 3 + dx;
-      const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx;
-      const float w10 = ly * (1.f - lx), w11 = ly * lx;
-      const float* z = p.z.ptr + (int64_t)n * p.z.sn + (int64_t)(tap * p.Co + c0) * p.z.sc;
-      const float* a = z + (int64_t)y0 * p.z.sh + (int64_t)x0 * p.z.sw;
-      const float* b = z + (int64_t)y0 * p.z.sh + (int64_t)x1 * p.z.sw;
-      const float* c = z + (int64_t)y1 * p.z.sh + (int64_t)x0 * p.z.sw;
-      const float* d = z + (int64_t)y1 * p.z.sh + (int64_t)x1 * p.z.sw;
-      if constexpr (VW == 4) {
-        const float4 A = *reinterpret_cast<const float4*>(a), B = *reinterpret_cast<const float4*>(b);
-        const float4 C = *reinterpret_cast<const float4*>(c), D = *reinterpret_cast<const float4*>(d);
-        acc[0] += w00 * A.x + w01 * B.x + w10 * C.x + w11 * D.x;
-        acc[1] += w00 * A.y + w01 * B.y + w10 * C.y + w11 * D.y;
-        acc[2] += w00 * A.z + w01 * B.z + w10 * C.z + w11 * D.z;
-        acc[3] += w00 * A.w + w01 * B.w + w10 * C.w + w11 * D.w;
-      } else {
-        acc[0] += w00 * a[0] + w01 * b[0] + w10 * c[0] + w11 * d[0];
-      }
+  for (int dx = 0; dx < 3; ++dx) {
+    const int xx = ox + dx - 1;
+    if ((unsigned)xx >= (unsigned)Wo) continue;
+    int x0, x1; float lx;
+    bilin_src(xx, Wi, Wo, p.ac, x0, x1, lx);
+    const float* z = p.z.ptr + (int64_t)n * p.z.sn + (int64_t)r * p.z.sh + (int64_t)((dy * 3 + dx) * p.Co + c0) * p.z.sc;
+    const float* a = z + (int64_t)x0 * p.z.sw;
+    const float* b = z + (int64_t)x1 * p.z.sw;
+    if constexpr (VW == 4) {
+      const float4 A = *reinterpret_cast<const float4*>(a), B = *reinterpret_cast<const float4*>(b);
+      h[0] += (1.f - lx) * A.x + lx * B.x;
+      h[1] += (1.f - lx) * A.y + lx * B.y;
+      h[2] += (1.f - lx) * A.z + lx * B.z;
+      h[3] += (1.f - lx) * A.w + lx * B.w;
+    } else {
+      h[0] += (1.f - lx) * a[0] + lx * b[0];
     }
   }
-  float out[VW];
+}
+
+template <int VW>
+__global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rblocks) {
+  const int chunk = blockIdx.x % p.chunks;
+  const int rb_n = blockIdx.x / p.chunks;
+  const int n = rb_n / rblocks, oy0 = (rb_n - n * rblocks) * R;
+  const int j = chunk * 256 + threadIdx.x;
+  if (j >= p.per_row) return;
+  const int cgroups = p.Co / VW;
+  const int ox = j / cgroups, c0 = (j - ox * cgroups) * VW;
+  const int Ho = p.y.h, Hi = p.z.h;
+  const int oy1 = oy0 + R < Ho ? oy0 + R : Ho;
+
+  float sc[VW], bi[VW], sl[VW];
 #pragma unroll
   for (int v = 0; v < VW; ++v) {
-    const int co = c0 + v;
-    const float s = p.scale ? p.scale[co] : 1.f;
-    const float bb = p.bias ? p.bias[co] : 0.f;
-    out[v] = apply_act(acc[v] * s + bb, p.act, p.slope ? p.slope[co] : 0.f);
+    sc[v] = p.scale ? p.scale[c0 + v] : 1.f;
+    bi[v] = p.bias ? p.bias[c0 + v] : 0.f;
+    sl[v] = p.slope ? p.slope[c0 + v] : 0.f;
   }
-  float* y = p.y.ptr + voff(p.y, n, oy, ox, c0);
-  if constexpr (VW == 4) {
-    if (p.y.sc == 1) {
-      *reinterpret_cast<float4*>(y) = make_float4(out[0], out[1], out[2], out[3]);
-      return;
-    }
-  }
+  float hA[3][VW], hB[3][VW];
+  int cur[3] = {-2, -2, -2};
+  float* yp = p.y.ptr + (int64_t)n * p.y.sn + (int64_t)ox * p.y.sw + (int64_t)c0 * p.y.sc;
+  for (int oy = oy0; oy < oy1; ++oy) {
+    float acc[VW];
 #pragma unroll
-  for (int v = 0; v < VW; ++v) y[(int64_t)v * p.y.sc] = out[v];
+    for (int v = 0; v < VW; ++v) acc[v] = 0.f;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const int yy = oy + dy - 1;
+      if ((unsigned)yy >= (unsigned)Ho) continue;
+      int y0, y1; float ly;
+      bilin_src(yy, Hi, Ho, p.ac, y0, y1, ly);
+      if (y0 != cur[dy]) {
+        if (y0 == cur[dy] + 1) {
+#pragma unroll
+          for (int v = 0; v < VW; ++v) hA[dy][v] = hB[dy][v];
+        } else {
+          up_hrow<VW>(p, n, y0, dy, ox, c0, hA[dy]);
+        }
+        up_hrow<VW>(p, n, y1, dy, ox, c0, hB[dy]);
+        cur[dy] = y0;
+      }
+#pragma unroll
+      for (int v = 0; v < VW; ++v) acc[v] += (1.f - ly) * hA[dy][v] + ly * hB[dy][v];
+    }
+    float out[VW];
+#pragma unroll
+    for (int v = 0; v < VW; ++v) out[v] = apply_act(acc[v] * sc[v] + bi[v], p.act, sl[v]);
+    float* y = yp + (int64_t)oy * p.y.sh;
+    if constexpr (VW == 4) {
+      if (p.y.sc == 1) {
+        *reinterpret_cast<float4*>(y) = make_float4(out[0], out[1], out[2], out[3]);
+        continue;
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < VW; ++v) y[(int64_t)v * p.y.sc] = out[v];
+  }
 }
 
 // Separable form of the same sum (6 loads per output instead of 36):
@@ -113,16 +153,15 @@ __global__ __launch_bounds__(256) void upconv3x3_kernel(UpK p) {
 // H is 3*Hi/Ho of the output's size and is re-read from L2 by every output row using it.
 template <int VW>
 __global__ __launch_bounds__(256) void upconv_h_kernel(UpK p, float* __restrict__ H) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= p.total) return;
+  int row, j;
+  row_pos(p.chunks, row, j);
+  if (j >= p.per_row) return;
   const int cgroups = p.Co / VW;
-  const int cg = (int)(t % cgroups);
-  int64_t q = t / cgroups;
+  const int ox = j / cgroups, cg = j - ox * cgroups;
   const int Wo = p.y.w, Hi = p.z.h, Wi = p.z.w;
-  const int ox = (int)(q % Wo); q /= Wo;
-  const int r = (int)(q % Hi); q /= Hi;
-  const int dy = (int)(q % 3);
-  const int n = (int)(q / 3);
+  // row = (n*3 + dy)*Hi + r
+  const int nd = row / Hi, r = row - nd * Hi;
+  const int n = nd / 3, dy = nd - n * 3;
   const int c0 = cg * VW;
   float acc[VW];
 #pragma unroll
@@ -146,22 +185,20 @@ __global__ __launch_bounds__(256) void upconv_h_kernel(UpK p, float* __restrict_
       acc[0] += (1.f - lx) * a[0] + lx * b[0];
     }
   }
-  float* h = H + ((((int64_t)n * 3 + dy) * Hi + r) * Wo + ox) * p.Co + c0;
+  float* h = H + ((int64_t)row * Wo + ox) * p.Co + c0;
   if constexpr (VW == 4) *reinterpret_cast<float4*>(h) = make_float4(acc[0], acc[1], acc[2], acc[3]);
   else h[0] = acc[0];
 }
 
 template <int VW>
 __global__ __launch_bounds__(256) void upconv_out_kernel(UpK p, const float* __restrict__ H) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= p.total) return;
+  int row, j;
+  row_pos(p.chunks, row, j);
+  if (j >= p.per_row) return;
   const int cgroups = p.Co / VW;
-  const int cg = (int)(t % cgroups);
-  int64_t q = t / cgroups;
+  const int ox = j / cgroups, cg = j - ox * cgroups;
   const int Ho = p.y.h, Wo = p.y.w, Hi = p.z.h;
-  const int ox = (int)(q % Wo); q /= Wo;
-  const int oy = (int)(q % Ho);
-  const int n = (int)(q / Ho);
+  const int n = row / Ho, oy = row - n * Ho;
   const int c0 = cg * VW;
   float acc[VW];
 #pragma unroll
@@ -209,17 +246,15 @@ struct DwK {
   prpe_view x, y, r;
   const float* w; int k, stride, pad;
   const float* scale; const float* bias; int act;
-  int64_t total;
+  int per_row, chunks;
 };
 __global__ __launch_bounds__(256) void dwconv_kernel(DwK p) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= p.total) return;
+  int row, j;
+  row_pos(p.chunks, row, j);
+  if (j >= p.per_row) return;
   const int C = p.y.c;
-  const int c = (int)(t % C);
-  int64_t q = t / C;
-  const int ow = (int)(q % p.y.w); q /= p.y.w;
-  const int oh = (int)(q % p.y.h);
-  const int n = (int)(q / p.y.h);
+  const int ow = j / C, c = j - ow * C;
+  const int n = row / p.y.h, oh = row - n * p.y.h;
   float acc = 0.f;
   const float* wc = p.w + (int64_t)c * p.k * p.k;
   for (int kh = 0; kh < p.k; ++kh) {
@@ -238,40 +273,50 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwK p) {
 }
 
 // ------------------------------------------------------------------------- maxpool
-struct PoolK { prpe_view x, y; int k, stride, pad; int64_t total; };
+struct PoolK { prpe_view x, y; int k, stride, pad; int per_row, chunks; };
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int VW>
 __global__ __launch_bounds__(256) void maxpool_kernel(PoolK p) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= p.total) return;
-  const int C = p.y.c;
-  const int c = (int)(t % C);
-  int64_t q = t / C;
-  const int ow = (int)(q % p.y.w); q /= p.y.w;
-  const int oh = (int)(q % p.y.h);
-  const int n = (int)(q / p.y.h);
-  float m = -INFINITY;
+  int row, j;
+  row_pos(p.chunks, row, j);
+  if (j >= p.per_row) return;
+  const int cg = p.y.c / VW;
+  const int ow = j / cg, c = (j - ow * cg) * VW;
+  const int n = row / p.y.h, oh = row - n * p.y.h;
+  float m[VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e) m[e] = -INFINITY;
   for (int kh = 0; kh < p.k; ++kh) {
     const int ih = oh * p.stride - p.pad + kh;
     if ((unsigned)ih >= (unsigned)p.x.h) continue;
     for (int kw = 0; kw < p.k; ++kw) {
       const int iw = ow * p.stride - p.pad + kw;
       if ((unsigned)iw >= (unsigned)p.x.w) continue;
-      const float v = p.x.ptr[voff(p.x, n, ih, iw, c)];
-      m = (v > m || v != v) ? v : m;   // NaN propagates like torch max_pool2d
+      const float* src = p.x.ptr + voff(p.x, n, ih, iw, c);
+      float v[VW];
+      if constexpr (VW == 4) {
+        const f4v q = *reinterpret_cast<const f4v*>(src);
+        v[0] = q[0]; v[1] = q[1]; v[2] = q[2]; v[3] = q[3];
+      } else {
+        v[0] = src[0];
+      }
+#pragma unroll
+      for (int e = 0; e < VW; ++e) m[e] = (v[e] > m[e] || v[e] != v[e]) ? v[e] : m[e];   // NaN propagates like torch
     }
   }
-  p.y.ptr[voff(p.y, n, oh, ow, c)] = m;
+  float* dst = p.y.ptr + voff(p.y, n, oh, ow, c);
+  if constexpr (VW == 4) *reinterpret_cast<f4v*>(dst) = f4v{m[0], m[1], m[2], m[3]};
+  else dst[0] = m[0];
 }
 
-struct Up2K { prpe_view x, y; int64_t total; };
+struct Up2K { prpe_view x, y; int per_row, chunks; };
 __global__ __launch_bounds__(256) void upsample2x_kernel(Up2K p) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= p.total) return;
+  int row, j;
+  row_pos(p.chunks, row, j);
+  if (j >= p.per_row) return;
   const int C = p.y.c;
-  const int c = (int)(t % C);
-  int64_t q = t / C;
-  const int ow = (int)(q % p.y.w); q /= p.y.w;
-  const int oh = (int)(q % p.y.h);
-  const int n = (int)(q / p.y.h);
+  const int ow = j / C, c = j - ow * C;
+  const int n = row / p.y.h, oh = row - n * p.y.h;
   p.y.ptr[voff(p.y, n, oh, ow, c)] = p.x.ptr[voff(p.x, n, oh >> 1, ow >> 1, c)];
 }
 
@@ -394,19 +439,27 @@ __global__ __launch_bounds__(256) void dfl_decode_kernel(DflK p) {
 // ------------------------------------------------------------------------- copy_pad
 // y[n,h,w,c] = c < x.c ? x[n,h,w,c] : 0  (layout change + channel zero-padding, e.g. NCHW
 // frames -> NHWC4 so the 7x7 stem takes the vectorised implicit-GEMM path)
-struct CopyK { prpe_view x, y; int64_t total; };
+struct CopyK { prpe_view x, y; int per_row, chunks; };
 __global__ __launch_bounds__(256) void copy_pad_kernel(CopyK p) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= p.total) return;
-  int64_t q = t;
-  const int w = (int)(q % p.y.w); q /= p.y.w;
-  const int h = (int)(q % p.y.h);
-  const int n = (int)(q / p.y.h);
+  int row, w;
+  row_pos(p.chunks, row, w);
+  if (w >= p.per_row) return;
+  const int n = row / p.y.h, h = row - n * p.y.h;
   float* y = p.y.ptr + voff(p.y, n, h, w, 0);
   for (int c = 0; c < p.y.c; ++c) y[(int64_t)c * p.y.sc] = c < p.x.c ? p.x.ptr[voff(p.x, n, h, w, c)] : 0.f;
 }
 
 inline unsigned nblocks(int64_t total, int bs = 256) { return (unsigned)((total + bs - 1) / bs); }
+
+// 1-D grid of rows * ceil(per_row / 256) blocks (see row_pos); false when it does not fit
+inline bool rowgrid(int64_t rows, int64_t per_row, dim3& g, int& chunks) {
+  if (rows <= 0 || per_row <= 0 || per_row >= (1LL << 30)) return false;
+  const int64_t c = (per_row + 255) / 256, total = rows * c;
+  if (total >= (1LL << 31)) return false;
+  chunks = (int)c;
+  g = dim3((unsigned)total);
+  return true;
+}
 
 }  // namespace
 
@@ -427,31 +480,33 @@ extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t al
                   (z->sn % 4 == 0) && ((uintptr_t)z->ptr % 16 == 0) &&
                   (y->sc != 1 || ((y->sw % 4 == 0) && (y->sh % 4 == 0) && (y->sn % 4 == 0) &&
                                   ((uintptr_t)y->ptr % 16 == 0)));
-  const int64_t pix = (int64_t)y->n * y->h * y->w;
   hipStream_t st = as_stream(stream);
+  const int VWs = v4 ? 4 : 1;
+  p.per_row = y->w * (y->c / VWs);
+  dim3 g_out, g_h;
+  if (!rowgrid((int64_t)y->n * y->h, p.per_row, g_out, p.chunks) ||
+      !rowgrid((int64_t)y->n * 3 * z->h, p.per_row, g_h, p.chunks))
+    return PRPE_EINVAL;
   const int64_t need = prpe_upconv3x3_workspace_bytes(z, y);
   if (workspace && workspace_bytes >= need && ((uintptr_t)workspace % 16) == 0) {
     float* H = static_cast<float*>(workspace);
-    const int VWs = v4 ? 4 : 1;
-    UpK ph = p;
-    ph.total = (int64_t)y->n * 3 * z->h * y->w * (y->c / VWs);
-    p.total = pix * (y->c / VWs);
     if (v4) {
-      hipLaunchKernelGGL(upconv_h_kernel<4>, dim3(nblocks(ph.total)), dim3(256), 0, st, ph, H);
-      hipLaunchKernelGGL(upconv_out_kernel<4>, dim3(nblocks(p.total)), dim3(256), 0, st, p, (const float*)H);
+      hipLaunchKernelGGL(upconv_h_kernel<4>, g_h, dim3(256), 0, st, p, H);
+      hipLaunchKernelGGL(upconv_out_kernel<4>, g_out, dim3(256), 0, st, p, (const float*)H);
     } else {
-      hipLaunchKernelGGL(upconv_h_kernel<1>, dim3(nblocks(ph.total)), dim3(256), 0, st, ph, H);
-      hipLaunchKernelGGL(upconv_out_kernel<1>, dim3(nblocks(p.total)), dim3(256), 0, st, p, (const float*)H);
+      hipLaunchKernelGGL(upconv_h_kernel<1>, g_h, dim3(256), 0, st, p, H);
+      hipLaunchKernelGGL(upconv_out_kernel<1>, g_out, dim3(256), 0, st, p, (const float*)H);
     }
     return launch_status();
   }
-  if (v4) {
-    p.total = pix * (y->c / 4);
-    hipLaunchKernelGGL(upconv3x3_kernel<4>, dim3(nblocks(p.total)), dim3(256), 0, st, p);
-  } else {
-    p.total = pix * y->c;
-    hipLaunchKernelGGL(upconv3x3_kernel<1>, dim3(nblocks(p.total)), dim3(256), 0, st, p);
-  }
+  // fused path: R output rows per thread; shrink R while the grid would not fill the chip
+  int R = 32;
+  while (R > 4 && (int64_t)y->n * ((y->h + R - 1) / R) * p.chunks < 8192) R /= 2;
+  const int rblocks = (y->h + R - 1) / R;
+  const int64_t nb = (int64_t)y->n * rblocks * p.chunks;
+  if (nb >= (1LL << 31)) return PRPE_EINVAL;
+  if (v4) hipLaunchKernelGGL(upconv_fused_kernel<4>, dim3((unsigned)nb), dim3(256), 0, st, p, R, rblocks);
+  else hipLaunchKernelGGL(upconv_fused_kernel<1>, dim3((unsigned)nb), dim3(256), 0, st, p, R, rblocks);
   return launch_status();
 }
 
@@ -465,15 +520,19 @@ extern "C" int prpe_dwconv(const prpe_view* x, const prpe_view* y, const prpe_vi
   p.x = *x; p.y = *y;
   if (res && res->ptr) p.r = *res;
   p.w = w; p.k = k; p.stride = stride; p.pad = pad; p.scale = scale; p.bias = bias; p.act = act;
-  p.total = (int64_t)y->n * y->h * y->w * y->c;
-  hipLaunchKernelGGL(dwconv_kernel, dim3(nblocks(p.total)), dim3(256), 0, as_stream(stream), p);
+  p.per_row = y->w * y->c;
+  dim3 g;
+  if (!rowgrid((int64_t)y->n * y->h, (int64_t)y->w * y->c, g, p.chunks)) return PRPE_EINVAL;
+  hipLaunchKernelGGL(dwconv_kernel, g, dim3(256), 0, as_stream(stream), p);
   return launch_status();
 }
 
 extern "C" int prpe_copy_pad(const prpe_view* x, const prpe_view* y, void* stream) {
   if (!view_ok(x) || !view_ok(y) || x->n != y->n || x->h != y->h || x->w != y->w || y->c < x->c) return PRPE_EINVAL;
-  CopyK p{*x, *y, (int64_t)y->n * y->h * y->w};
-  hipLaunchKernelGGL(copy_pad_kernel, dim3(nblocks(p.total)), dim3(256), 0, as_stream(stream), p);
+  CopyK p{*x, *y, y->w, 0};
+  dim3 g;
+  if (!rowgrid((int64_t)y->n * y->h, y->w, g, p.chunks)) return PRPE_EINVAL;
+  hipLaunchKernelGGL(copy_pad_kernel, g, dim3(256), 0, as_stream(stream), p);
   return launch_status();
 }
 
@@ -481,16 +540,26 @@ extern "C" int prpe_maxpool(const prpe_view* x, const prpe_view* y, int32_t k, i
                             void* stream) {
   if (!view_ok(x) || !view_ok(y) || x->c != y->c || x->n != y->n || k <= 0 || stride <= 0) return PRPE_EINVAL;
   if ((x->h + 2 * pad - k) / stride + 1 != y->h || (x->w + 2 * pad - k) / stride + 1 != y->w) return PRPE_EINVAL;
-  PoolK p{*x, *y, k, stride, pad, (int64_t)y->n * y->h * y->w * y->c};
-  hipLaunchKernelGGL(maxpool_kernel, dim3(nblocks(p.total)), dim3(256), 0, as_stream(stream), p);
+  auto a16 = [](const prpe_view* v) {
+    return v->sc == 1 && v->c % 4 == 0 && v->sw % 4 == 0 && v->sh % 4 == 0 && v->sn % 4 == 0 &&
+           ((uintptr_t)v->ptr % 16) == 0;
+  };
+  const bool v4 = a16(x) && a16(y);
+  PoolK p{*x, *y, k, stride, pad, y->w * (y->c / (v4 ? 4 : 1)), 0};
+  dim3 g;
+  if (!rowgrid((int64_t)y->n * y->h, p.per_row, g, p.chunks)) return PRPE_EINVAL;
+  if (v4) hipLaunchKernelGGL(maxpool_kernel<4>, g, dim3(256), 0, as_stream(stream), p);
+  else hipLaunchKernelGGL(maxpool_kernel<1>, g, dim3(256), 0, as_stream(stream), p);
   return launch_status();
 }
 
 extern "C" int prpe_upsample_nearest2x(const prpe_view* x, const prpe_view* y, void* stream) {
   if (!view_ok(x) || !view_ok(y) || x->c != y->c || x->n != y->n || y->h != 2 * x->h || y->w != 2 * x->w)
     return PRPE_EINVAL;
-  Up2K p{*x, *y, (int64_t)y->n * y->h * y->w * y->c};
-  hipLaunchKernelGGL(upsample2x_kernel, dim3(nblocks(p.total)), dim3(256), 0, as_stream(stream), p);
+  Up2K p{*x, *y, y->w * y->c, 0};
+  dim3 g;
+  if (!rowgrid((int64_t)y->n * y->h, (int64_t)y->w * y->c, g, p.chunks)) return PRPE_EINVAL;
+  hipLaunchKernelGGL(upsample2x_kernel, g, dim3(256), 0, as_stream(stream), p);
   return launch_status();
 }
 

@@ -56,7 +56,8 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
     return y
 
 
-def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none", separable=True):
+def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none", separable=False):
+    """Fused one-pass kernel by default; ``separable=True`` runs the two-pass workspace form."""
     zv, yv = view(z), view(y)
     ws, nbytes = None, 0
     if separable:

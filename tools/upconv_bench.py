@@ -1,0 +1,68 @@
+"""Micro-benchmark of prpe_upconv3x3 (fused one-pass and separable) on the adapters' shapes (GPU box).
+
+    python tools/upconv_bench.py [--batch 32]
+
+Prints ms and effective GB/s (algorithmic bytes: z read + y write [+ H write+read]) next to a
+plain device copy of the output size as the bandwidth reference.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "person-recognition-for-pose-estimation_amd")]
+
+import torch  # noqa: E402
+
+from prpe import ops  # noqa: E402
+
+# name: (Hi, Wi, Ho, Wo, Co, align_corners, act)
+SHAPES = {
+    "yolo_adapter.4 20->160 Co512": (20, 20, 160, 160, 512, True, "silu"),
+    "ada_adapter.4 20->112 Co512": (20, 20, 112, 112, 512, True, "prelu"),
+    "vit_adapter.4 20->256x192 Co256": (20, 20, 256, 192, 256, True, "gelu"),
+    "vit head 16x12->64x48 Co17": (16, 12, 64, 48, 17, False, "none"),
+}
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    dev = "cuda"
+    B = a.batch
+    for name, (Hi, Wi, Ho, Wo, Co, ac, act) in SHAPES.items():
+        z = torch.rand(B, Hi, Wi, 9 * Co, device=dev)
+        y = torch.empty(B, Ho, Wo, Co, device=dev)
+        y2 = torch.empty_like(y)
+        sc = torch.rand(Co, device=dev) + 0.5
+        bi = torch.rand(Co, device=dev)
+        sl = torch.rand(Co, device=dev) * 0.3
+        ybytes = y.numel() * 4
+        hbytes = 3 * B * Hi * Wo * Co * 4
+        ms_copy = timeit(lambda: y2.copy_(y), a.iters)
+        print(f"{name:34s} copy(y)            {ms_copy:8.3f} ms  {2 * ybytes / ms_copy / 1e6:8.1f} GB/s", flush=True)
+        for sep in (True, False):
+            for variant in ("plain", "epi"):
+                kw = dict(scale=sc, bias=bi, slope=sl if act == "prelu" else None, act=act) if variant == "epi" else {}
+                ms = timeit(lambda: ops.upconv3x3(z, y, ac, separable=sep, **kw), a.iters)
+                alg = z.numel() * 4 + ybytes + (2 * hbytes if sep else 0)
+                print(f"{name:34s} {'sep' if sep else 'fused':6s} {variant:5s}       {ms:8.3f} ms  "
+                      f"{alg / ms / 1e6:8.1f} GB/s  (y write {ybytes / ms / 1e6:8.1f} GB/s)", flush=True)
+
+
+if __name__ == "__main__":
+    main()
