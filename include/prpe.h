@@ -79,7 +79,7 @@ typedef struct prpe_conv_desc {
   const float* scale;     /* [Co] or NULL (= 1) */
   const float* bias;      /* [Co] or NULL (= 0) */
   const float* slope;     /* [Co] PReLU slopes or NULL */
-  const float* in_scale;  /* [Ci] or NULL */
+  const float* in_scale;  /* [Ci] or NULL; needs the vector path (x.sc == 1, Ci % 4 == 0, 16-B rows) */
   const float* in_bias;   /* [Ci] or NULL */
   int32_t act;            /* prpe_act */
   int32_t res_mode;       /* prpe_res_mode */

@@ -136,6 +136,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
 
   f4 areg[VEC ? A_ROWS_PT : 1];
   float sreg[VEC ? 1 : S_KPT];
+  unsigned amask = 0;                                // in-bounds bits of areg / sreg
+  f4 as4 = {1.f, 1.f, 1.f, 1.f}, ab4 = {0.f, 0.f, 0.f, 0.f};   // prologue affine of this K-step
+  static_assert(A_ROWS_PT <= 32 && S_KPT <= 32, "amask");
   u4 breg[NP][B_PT];
 
   auto load_tile = [&](int kt) {
@@ -151,20 +154,24 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
         kh = c_kh; kw = c_kw; ci = c_ci;
         kval = c_kh < p.KH;
       }
-      f4 s4 = {1.f, 1.f, 1.f, 1.f}, b4 = {0.f, 0.f, 0.f, 0.f};
-      if (p.in_scale && kval) {
-        s4 = *reinterpret_cast<const f4*>(p.in_scale + ci);
-        b4 = *reinterpret_cast<const f4*>(p.in_bias + ci);
+      // Branch-free gather: out-of-bounds rows load from the (valid) base pointer and are
+      // zeroed in store_tile through amask. Nothing here consumes a loaded value, so the
+      // loads stay in flight across compute() -- a value used right after its load (the
+      // prologue affine used to be applied here) makes the compiler wait for every load
+      // before the MFMAs start.
+      if (p.in_scale) {
+        const int cs = kval ? ci : 0;
+        as4 = *reinterpret_cast<const f4*>(p.in_scale + cs);
+        ab4 = *reinterpret_cast<const f4*>(p.in_bias + cs);
       }
+      amask = 0;
 #pragma unroll
       for (int i = 0; i < A_ROWS_PT; ++i) {
         const int ih = ih0[i] + kh, iw = iw0[i] + kw;
-        f4 v = {0.f, 0.f, 0.f, 0.f};
-        if (kval && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) {
-          v = *reinterpret_cast<const f4*>(p.x + rowoff[i] + ih * p.xsh + iw * p.xsw + ci);
-          if (p.in_scale) v = v * s4 + b4;
-        }
-        areg[i] = v;
+        const bool ok = kval && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+        const float* src = ok ? p.x + rowoff[i] + ih * p.xsh + iw * p.xsw + ci : p.x;
+        areg[i] = *reinterpret_cast<const f4*>(src);
+        amask |= (unsigned)ok << i;
       }
       if constexpr (KM == 1) {
         c_ci += BK;
@@ -173,20 +180,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
     } else {
       const int kk0 = tid / BM;
       constexpr int KSTEP = NT / BM;
+      amask = 0;
 #pragma unroll
       for (int j = 0; j < S_KPT; ++j) {
         const int k = kt * BK + kk0 + KSTEP * j;
         const int e = klut[k];
-        float v = 0.f;
-        if (e >= 0) {
-          const int dh = e >> 24, dw = (e >> 16) & 0xFF, ci = e & 0xFFFF;
-          const int ih = ih0[0] + dh, iw = iw0[0] + dw;
-          if ((unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi) {
-            v = p.x[rowoff[0] + ih * p.xsh + iw * p.xsw + ci * p.xsc];
-            if (p.in_scale) v = v * p.in_scale[ci] + p.in_bias[ci];
-          }
-        }
-        sreg[j] = v;
+        const int dh = e >> 24, dw = (e >> 16) & 0xFF, ci = e & 0xFFFF;
+        const int ih = ih0[0] + dh, iw = iw0[0] + dw;
+        const bool ok = e >= 0 && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+        sreg[j] = *(ok ? p.x + rowoff[0] + ih * p.xsh + iw * p.xsw + ci * p.xsc : p.x);
+        amask |= (unsigned)ok << j;
       }
     }
     // B: packed planes [co_pad][k_pad] bf16
@@ -197,8 +200,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
         const int row = c >> 2, ch = c & 3;
         const int64_t off = (int64_t)(n0 + row) * p.k_pad + kt * BK + ch * 8;
         breg[0][j] = *reinterpret_cast<const u4*>(p.whi + off);
-        if (NP > 1) breg[1][j] = *reinterpret_cast<const u4*>(p.wlo + off);
-        if (NP > 2) breg[NP - 1][j] = *reinterpret_cast<const u4*>(p.wlo2 + off);
+        if constexpr (NP > 1) breg[1][j] = *reinterpret_cast<const u4*>(p.wlo + off);
+        if constexpr (NP > 2) breg[NP - 1][j] = *reinterpret_cast<const u4*>(p.wlo2 + off);
       }
     }
   };
@@ -212,7 +215,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
         const int slot = (c4 >> 1) ^ swzF(row);
         const int off = row * BK + slot * 8 + (c4 & 1) * 4;
         bf16x4 pl[NP];
-        const f4 v = areg[i];
+        f4 v = areg[i];
+        if (p.in_scale) v = v * as4 + ab4;
+        if (!((amask >> i) & 1u)) v = f4{0.f, 0.f, 0.f, 0.f};   // padding stays 0 (no prologue)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float r = v[e];
@@ -234,7 +239,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
         const int kk = kk0 + KSTEP * j;
         const int slot = (kk >> 3) ^ swzF(row);
         const int off = row * BK + slot * 8 + (kk & 7);
-        float r = sreg[j];
+        float r = ((amask >> j) & 1u) ? sreg[j] : 0.f;
 #pragma unroll
         for (int q = 0; q < NP; ++q) {
           const __bf16 t = (__bf16)r;
@@ -332,24 +337,43 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
       __syncthreads();
       if (col < p.Co) {
         const int rows = BM - h0 < CH ? BM - h0 : CH;
-        for (int rr = tid / CPR; rr < rows; rr += RPP) {
-          const int m = m0 + h0 + rr;
-          if (m >= p.M) break;
-          const int n = m / p.HoWo;
-          const int rem = m - n * p.HoWo;
-          const int oh = rem / p.Wo;
-          const int ow = rem - oh * p.Wo;
-          f4 v = *reinterpret_cast<const f4*>(ct + rr * CS + cc * 4);
-          v = v * sc4 + bi4;
-          f4 res = {0.f, 0.f, 0.f, 0.f};
-          if (p.res_mode != PRPE_RES_NONE)
-            res = *reinterpret_cast<const f4*>(p.r + (int64_t)n * p.rsn + (int64_t)oh * p.rsh +
-                                              (int64_t)ow * p.rsw + col);
-          if (p.res_mode == PRPE_RES_PRE_ACT) v += res;
+        // EB rows per batch: all residual loads of a batch are issued before the first store
+        // (y and r are distinct buffers, but the compiler cannot know that and would otherwise
+        // serialise load -> store -> load on every row)
+        constexpr int EB = 4;
+        for (int rb = tid / CPR; rb < rows; rb += RPP * EB) {
+          int64_t yo[EB];
+          f4 res[EB];
+          bool ok[EB];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act, sl4[e]);
-          if (p.res_mode == PRPE_RES_POST_ACT) v += res;
-          *reinterpret_cast<f4*>(p.y + (int64_t)n * p.ysn + (int64_t)oh * p.ysh + (int64_t)ow * p.ysw + col) = v;
+          for (int e = 0; e < EB; ++e) {
+            const int rr = rb + RPP * e;
+            const int m = m0 + h0 + rr;
+            ok[e] = rr < rows && m < p.M;
+            res[e] = f4{0.f, 0.f, 0.f, 0.f};
+            yo[e] = 0;
+            if (ok[e]) {
+              const int n = m / p.HoWo;
+              const int rem = m - n * p.HoWo;
+              const int oh = rem / p.Wo;
+              const int ow = rem - oh * p.Wo;
+              yo[e] = (int64_t)n * p.ysn + (int64_t)oh * p.ysh + (int64_t)ow * p.ysw + col;
+              if (p.res_mode != PRPE_RES_NONE)
+                res[e] = *reinterpret_cast<const f4*>(p.r + (int64_t)n * p.rsn + (int64_t)oh * p.rsh +
+                                                      (int64_t)ow * p.rsw + col);
+            }
+          }
+#pragma unroll
+          for (int e = 0; e < EB; ++e) {
+            if (!ok[e]) continue;
+            f4 v = *reinterpret_cast<const f4*>(ct + (rb + RPP * e) * CS + cc * 4);
+            v = v * sc4 + bi4;
+            if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
+            if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
+            *reinterpret_cast<f4*>(p.y + yo[e]) = v;
+          }
         }
       }
       if (h0 + CH < BM) __syncthreads();
@@ -518,6 +542,8 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   if (d->k_order == 1 && (!vec || x.c % 32 != 0)) return PRPE_EINVAL;
   const int km = d->k_order == 1 ? 2 : (vec ? 1 : 0);
   if (km == 0 && d->k_pad > 1024) return PRPE_EINVAL;
+  // the input-side affine is implemented on the vector paths only (IR-50 pre-BN, Ci >= 64)
+  if (km == 0 && d->in_scale) return PRPE_EINVAL;
 
   ConvK kp{};
   kp.x = x.ptr; kp.xsn = x.sn; kp.xsh = x.sh; kp.xsw = x.sw; kp.xsc = x.sc;

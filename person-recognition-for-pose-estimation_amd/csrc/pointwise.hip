@@ -386,6 +386,53 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* x, int64_t 
   }
 }
 
+// register-resident variant: the row is read once (NV float4 per lane, C % 4 == 0,
+// C <= 256*NV, 16-B aligned rows), statistics from registers, one write
+template <int NV>
+__global__ __launch_bounds__(256) void layernorm_reg_kernel(const float* __restrict__ x, int64_t xs,
+                                                            float* __restrict__ y, int64_t ys, int64_t rows, int C,
+                                                            const float* __restrict__ g,
+                                                            const float* __restrict__ b, float eps, int relu) {
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int lane = threadIdx.x & 63;
+  const float* xr = x + row * xs;
+  f4v v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    v[i] = c < C ? *reinterpret_cast<const f4v*>(xr + c) : f4v{0.f, 0.f, 0.f, 0.f};
+    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+  const float mean = warp_sum(s) / (float)C;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < C) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { const float d = v[i][e] - mean; q += d * d; }
+    }
+  }
+  const float var = warp_sum(q) / (float)C;
+  const float rstd = 1.f / sqrtf(var + eps);
+  float* yr = y + row * ys;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = (i * 64 + lane) * 4;
+    if (c < C) {
+      const f4v gg = *reinterpret_cast<const f4v*>(g + c), bb = *reinterpret_cast<const f4v*>(b + c);
+      f4v o = (v[i] - mean) * rstd * gg + bb;
+      if (relu) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = o[e] > 0.f ? o[e] : 0.f;
+      }
+      *reinterpret_cast<f4v*>(yr + c) = o;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------- l2norm
 __global__ __launch_bounds__(256) void l2norm_kernel(const float* x, float* emb, float* norm, int rows, int C) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -574,6 +621,14 @@ extern "C" int prpe_norm_sigmoid(const prpe_view* x, const prpe_view* y, void* s
 extern "C" int prpe_layernorm(const float* x, int64_t xs, float* y, int64_t ys, int64_t rows, int32_t C,
                               const float* g, const float* b, float eps, int32_t relu, void* stream) {
   if (!x || !y || !g || !b || rows <= 0 || C <= 0) return PRPE_EINVAL;
+  const bool al = C % 4 == 0 && xs % 4 == 0 && ys % 4 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
+                  (uintptr_t)g % 16 == 0 && (uintptr_t)b % 16 == 0;
+  const dim3 grid((unsigned)((rows + 3) / 4));
+  hipStream_t st = as_stream(stream);
+  if (al && C <= 256) { hipLaunchKernelGGL(layernorm_reg_kernel<1>, grid, dim3(256), 0, st, x, xs, y, ys, rows, C, g, b, eps, relu); return launch_status(); }
+  if (al && C <= 512) { hipLaunchKernelGGL(layernorm_reg_kernel<2>, grid, dim3(256), 0, st, x, xs, y, ys, rows, C, g, b, eps, relu); return launch_status(); }
+  if (al && C <= 768) { hipLaunchKernelGGL(layernorm_reg_kernel<3>, grid, dim3(256), 0, st, x, xs, y, ys, rows, C, g, b, eps, relu); return launch_status(); }
+  if (al && C <= 1024) { hipLaunchKernelGGL(layernorm_reg_kernel<4>, grid, dim3(256), 0, st, x, xs, y, ys, rows, C, g, b, eps, relu); return launch_status(); }
   hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, as_stream(stream), x, xs, y,
                      ys, rows, C, g, b, eps, relu);
   return launch_status();

@@ -333,14 +333,16 @@ def test_norm_sigmoid():
 
 
 @pytest.mark.parametrize("relu", [False, True])
-def test_layernorm(relu):
-    x = rnd(384, 768, seed=39, scale=4.0) + 1.0
-    g = torch.rand(768, generator=_g(40)) + 0.5
-    b = rnd(768, seed=41)
-    y = torch.empty(384, 768, device=DEV)
+@pytest.mark.parametrize("C", [768, 200, 1000, 770])
+def test_layernorm(relu, C):
+    """register-resident kernel (C % 4 == 0, C <= 1024) and the generic one (C = 770)"""
+    x = rnd(384, C, seed=39, scale=4.0) + 1.0
+    g = torch.rand(C, generator=_g(40)) + 0.5
+    b = rnd(C, seed=41)
+    y = torch.empty(384, C, device=DEV)
     ops.layernorm(x.to(DEV), y, g.to(DEV), b.to(DEV), 1e-12, relu)
     torch.cuda.synchronize()
-    ref = F.layer_norm(x, (768,), g, b, 1e-12)
+    ref = F.layer_norm(x, (C,), g, b, 1e-12)
     if relu:
         ref = F.relu(ref)
     torch.testing.assert_close(y.cpu(), ref, rtol=0, atol=1e-5)

@@ -22,6 +22,8 @@ SHAPES = {
     "yolo_adapter.10 3x3 256->128 @160": (160, 160, 256, 128, 3, 1, 1),
     "trunk l1 3x3 64->64 @160": (160, 160, 64, 64, 3, 1, 1),
     "trunk l1 1x1 64->256 @160": (160, 160, 64, 256, 1, 1, 0),
+    "trunk l1 conv3 1x1 64->256 +res @160": (160, 160, 64, 256, 1, 1, 0, "res"),
+    "trunk stem 7x7/2 4->64 @640": (640, 640, 4, 64, 7, 2, 3),
     "trunk l1 1x1 256->64 @160": (160, 160, 256, 64, 1, 1, 0),
     "trunk l3 3x3 256->256 @40": (40, 40, 256, 256, 3, 1, 1),
     "trunk l3 1x1 1024->256 @40": (40, 40, 1024, 256, 1, 1, 0),
@@ -42,7 +44,7 @@ def main():
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
-    for name, (H, W, Ci, Co, k, s, p) in SHAPES.items():
+    for name, (H, W, Ci, Co, k, s, p, *flags) in SHAPES.items():
         if a.only and a.only not in name:
             continue
         B = a.batch
@@ -56,16 +58,17 @@ def main():
                                      k_order=ko)
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         y = torch.empty(B, Ho, Wo, Co, device=dev)
+        r = torch.rand(B, Ho, Wo, Co, device=dev) if "res" in flags else None
         fl = 2.0 * B * Ho * Wo * Co * Ci * k * k
         for (ko, pk) in pks.items():
           for prec in [int(v) for v in a.prec.split(",")]:
             for tile in [int(v) for v in a.tiles.split(",")]:
-                ops.conv2d(x, pk, y, precision=prec, tile=tile)
+                ops.conv2d(x, pk, y, res=r, res_mode=1 if r is not None else 0, precision=prec, tile=tile)
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
-                    ops.conv2d(x, pk, y, precision=prec, tile=tile)
+                    ops.conv2d(x, pk, y, res=r, res_mode=1 if r is not None else 0, precision=prec, tile=tile)
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.iters
