@@ -189,6 +189,27 @@ int prpe_softargmax(const float* heat, int32_t B, int32_t K, int32_t H, int32_t 
                     const float* boxes, float* coords, float* scores, int32_t* argmax,
                     void* stream);
 
+/*
+ * Pose flip test, device half (pose_estimation/module.py:470-484):
+ *   out = (heat + F) * 0.5,  F[b,k,h,w] = heat_flipped[b', k', h, W-1-w]
+ * heat_flipped = heatmaps of the W-flipped frames. partner[k] (host, K <= 64) = the other
+ * keypoint of k's flip pair or -1. mode 0 = the reference's arithmetic: for paired channels
+ * ``flipped[:, pair].flip(0)`` reverses the BATCH order (b' = B-1-b, k' = k); mode 1 = the
+ * channel swap the code intends (b' = b, k' = partner[k]). out must not alias heat_flipped.
+ */
+int prpe_flip_average(const float* heat, const float* heat_flipped, float* out, int32_t B, int32_t K,
+                      int32_t H, int32_t W, const int32_t* partner, int32_t mode, void* stream);
+
+/*
+ * Face-recognition eval head, row reductions (face_recognition/module.py:141-145):
+ * logits [B, C] (row stride ld) = s * cos(normalize(emb), normalize(kernel)) from prpe_conv2d.
+ * argmax[b] = first index of the row max (torch.max(1)[1]); with labels (int64 [B]):
+ * loss[b] = logsumexp(row) - row[label]; summary (optional, [2]) = mean loss
+ * (F.cross_entropy) and mean(argmax == label) (the reference's acc).
+ */
+int prpe_ce_argmax(const float* logits, int64_t ld, int32_t B, int32_t C, const int64_t* labels,
+                   float* loss, int32_t* argmax, float* summary, void* stream);
+
 /* ABI version / build info. */
 int prpe_abi_version(void);
 const char* prpe_build_info(void);

@@ -387,3 +387,33 @@ def oks_delta(coords_a: Tensor, coords_b: Tensor, h=256, w=192) -> float:
     area = float(h * w)
     oks = torch.exp(-d2 / (2 * area * (2 * s) ** 2)).mean(-1)
     return float((1 - oks).max())
+
+
+# ---------------------------------------------------------------- eval steps
+COCO_FLIP_PAIRS = [(1, 2), (3, 4), (5, 6), (7, 8), (9, 10), (11, 12), (13, 14), (15, 16)]  # datamodule.py:25-34
+
+
+def pose_flip_average(pred_heatmaps: Tensor, flipped_output_heatmaps: Tensor, mode: str = "reference") -> Tensor:
+    """pose_estimation/module.py:476-484: flip the flipped pass's heatmaps back along W, apply
+    the pair handling, average. ``reference`` keeps the code's ``[:, pair].flip(0)`` (a batch
+    reversal of the paired channels); ``swap`` exchanges the pair's channels instead."""
+    flipped = torch.flip(flipped_output_heatmaps, dims=[-1])
+    for pair in COCO_FLIP_PAIRS:
+        if mode == "reference":
+            flipped[:, pair] = flipped[:, pair].flip(0)
+        else:
+            flipped[:, pair] = flipped[:, pair].flip(1)
+    return (pred_heatmaps + flipped) * 0.5
+
+
+def face_recognition_eval(embeddings: Tensor, head_kernel: Tensor, labels: Tensor, s: float = 64.0):
+    """face_recognition/module.py:137-145: cosine logits against the row-normalised head
+    kernel (F.normalize default dim=1 on the [512, classes] kernel), scaled by s, then
+    cross-entropy and top-1 accuracy. Returns (loss, acc, output, argmax)."""
+    kernel = F.normalize(head_kernel)
+    cosine = F.linear(F.normalize(embeddings), kernel.t())
+    output = cosine * s
+    loss = F.cross_entropy(output, labels)
+    amax = output.max(1)[1]
+    acc = (amax == labels).float().mean()
+    return loss, acc, output, amax

@@ -56,7 +56,12 @@ typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 // KM: 0 = scalar gather through a k -> (kh,kw,ci) LUT (any Ci, e.g. 3-channel inputs)
 //     1 = vector loads, tap-major K (Ci % 4 == 0)
 //     2 = vector loads, chunk-major K (Ci % 32 == 0, weights packed with k_order 1)
-template <int BM, int BN, int WM, int WN, int KM, int PREC>
+// PRO: input-side affine (IR-50 pre-BN) compiled in; vector paths only.
+// VALU budget (the MFMAs of a K-step are 48 / 96 per wave at 2 / 3 planes): the per-row gather
+// costs a bit test, a select and one 64-bit add -- row bases and the tap validity of every row
+// (one bit per kh and per kw) are computed once, the K-step offset is wave-uniform (KM 2) or
+// advanced incrementally (KM 1).
+template <int BM, int BN, int WM, int WN, int KM, int PREC, bool PRO>
 __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
   constexpr int NT = 64 * WM * WN;
   constexpr bool VEC = KM != 0;
@@ -94,6 +99,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
   constexpr int S_KPT = (BM * BK) / NT;               // scalar: k elements per thread per step
   int64_t rowoff[VEC ? A_ROWS_PT : 1];
   int ih0[VEC ? A_ROWS_PT : 1], iw0[VEC ? A_ROWS_PT : 1];
+  int64_t rbase[VEC ? A_ROWS_PT : 1];                 // element offset of tap (0,0), may be < 0
+  unsigned hmask[VEC ? A_ROWS_PT : 1], wmask[VEC ? A_ROWS_PT : 1];   // in-bounds kh / kw bits
 
   auto decode_row = [&](int m, int64_t& off, int& ih, int& iw) {
     if (m < p.M) {
@@ -111,7 +118,15 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
 
   if constexpr (VEC) {
 #pragma unroll
-    for (int i = 0; i < A_ROWS_PT; ++i) decode_row(m0 + (tid >> 3) + RPASS * i, rowoff[i], ih0[i], iw0[i]);
+    for (int i = 0; i < A_ROWS_PT; ++i) {
+      decode_row(m0 + (tid >> 3) + RPASS * i, rowoff[i], ih0[i], iw0[i]);
+      rbase[i] = rowoff[i] + (int64_t)ih0[i] * p.xsh + (int64_t)iw0[i] * p.xsw;
+      unsigned hm = 0, wmk = 0;
+      for (int t = 0; t < p.KH; ++t) hm |= (unsigned)((unsigned)(ih0[i] + t) < (unsigned)p.Hi) << t;
+      for (int t = 0; t < p.KW; ++t) wmk |= (unsigned)((unsigned)(iw0[i] + t) < (unsigned)p.Wi) << t;
+      hmask[i] = hm;
+      wmask[i] = wmk;
+    }
   } else {
     decode_row(m0 + (tid % BM), rowoff[0], ih0[0], iw0[0]);
     // k -> packed (dh, dw, ci) table for this layer (k_pad <= 1024 checked on host)
@@ -127,12 +142,24 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
     __syncthreads();
   }
 
-  // KM 1: incremental (kh, kw, ci) of this thread's chunk
+  // KM 1: incremental (kh, kw, ci) of this thread's chunk and its element offset
   int c_ci = (tid & 7) * 4, c_kh = 0, c_kw = 0;
+  int64_t c_off = 0;
+  auto c_advance = [&]() {   // carry c_ci >= Ci into kw / kh
+    while (c_ci >= p.Ci && c_kh < p.KH) {
+      c_ci -= p.Ci;
+      c_off += p.xsw - p.Ci;
+      if (++c_kw == p.KW) { c_kw = 0; ++c_kh; c_off += p.xsh - (int64_t)p.KW * p.xsw; }
+    }
+  };
   if constexpr (KM == 1) {
-    while (c_ci >= p.Ci) { c_ci -= p.Ci; if (++c_kw == p.KW) { c_kw = 0; ++c_kh; } }
+    c_off = c_ci;
+    c_advance();
   }
-  const int khw = p.KH * p.KW;
+  // KM 2: wave-uniform (chunk, kh, kw) of the next K-step to load
+  int u_kh = 0, u_kw = 0, u_ci = 0;                   // u_ci = chunk*32
+  int64_t u_off = 0;                                  // kh*xsh + kw*xsw + chunk*32
+  const int cthr = (tid & 7) * 4;
 
   f4 areg[VEC ? A_ROWS_PT : 1];
   float sreg[VEC ? 1 : S_KPT];
@@ -143,39 +170,43 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
 
   auto load_tile = [&](int kt) {
     if constexpr (VEC) {
-      int kh, kw, ci;
+      int kh, kw;
+      int64_t off;
       bool kval;
       if constexpr (KM == 2) {
-        const int chunk = kt / khw, tap = kt - chunk * khw;
-        kh = tap / p.KW; kw = tap - kh * p.KW;
-        ci = chunk * BK + (tid & 7) * 4;
+        kh = u_kh; kw = u_kw; off = u_off + cthr;
         kval = true;
+        if constexpr (PRO) {
+          as4 = *reinterpret_cast<const f4*>(p.in_scale + u_ci + cthr);
+          ab4 = *reinterpret_cast<const f4*>(p.in_bias + u_ci + cthr);
+        }
+        // next K-step: kw, then kh, then the next 32-channel chunk
+        u_off += p.xsw;
+        if (++u_kw == p.KW) {
+          u_kw = 0; u_off += p.xsh - (int64_t)p.KW * p.xsw;
+          if (++u_kh == p.KH) { u_kh = 0; u_ci += BK; u_off += BK - (int64_t)p.KH * p.xsh; }
+        }
       } else {
-        kh = c_kh; kw = c_kw; ci = c_ci;
+        kh = c_kh; kw = c_kw; off = c_off;
         kval = c_kh < p.KH;
+        if constexpr (PRO) {
+          const int cs = kval ? c_ci : 0;
+          as4 = *reinterpret_cast<const f4*>(p.in_scale + cs);
+          ab4 = *reinterpret_cast<const f4*>(p.in_bias + cs);
+        }
+        c_ci += BK;
+        c_off += BK;
+        c_advance();
       }
-      // Branch-free gather: out-of-bounds rows load from the (valid) base pointer and are
-      // zeroed in store_tile through amask. Nothing here consumes a loaded value, so the
-      // loads stay in flight across compute() -- a value used right after its load (the
-      // prologue affine used to be applied here) makes the compiler wait for every load
-      // before the MFMAs start.
-      if (p.in_scale) {
-        const int cs = kval ? ci : 0;
-        as4 = *reinterpret_cast<const f4*>(p.in_scale + cs);
-        ab4 = *reinterpret_cast<const f4*>(p.in_bias + cs);
-      }
+      // Branch-free gather: out-of-bounds rows load element 0 and are zeroed in store_tile
+      // through amask. Nothing here consumes a loaded value, so the loads stay in flight
+      // across compute().
       amask = 0;
 #pragma unroll
       for (int i = 0; i < A_ROWS_PT; ++i) {
-        const int ih = ih0[i] + kh, iw = iw0[i] + kw;
-        const bool ok = kval && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
-        const float* src = ok ? p.x + rowoff[i] + ih * p.xsh + iw * p.xsw + ci : p.x;
-        areg[i] = *reinterpret_cast<const f4*>(src);
+        const bool ok = kval && ((hmask[i] >> kh) & (wmask[i] >> kw) & 1u);
+        areg[i] = *reinterpret_cast<const f4*>(p.x + (ok ? rbase[i] + off : 0));
         amask |= (unsigned)ok << i;
-      }
-      if constexpr (KM == 1) {
-        c_ci += BK;
-        while (c_ci >= p.Ci && c_kh < p.KH) { c_ci -= p.Ci; if (++c_kw == p.KW) { c_kw = 0; ++c_kh; } }
       }
     } else {
       const int kk0 = tid / BM;
@@ -216,7 +247,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
         const int off = row * BK + slot * 8 + (c4 & 1) * 4;
         bf16x4 pl[NP];
         f4 v = areg[i];
-        if (p.in_scale) v = v * as4 + ab4;
+        if constexpr (PRO) v = v * as4 + ab4;
         if (!((amask >> i) & 1u)) v = f4{0.f, 0.f, 0.f, 0.f};   // padding stays 0 (no prologue)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -492,12 +523,12 @@ __global__ __launch_bounds__(256) void conv_smallco_kernel(ConvK p, int lpp_log2
   }
 }
 
-template <int BM, int BN, int WM, int WN, int KM>
+template <int BM, int BN, int WM, int WN, int KM, bool PRO>
 int launch_km(const ConvK& kp, int prec, dim3 grid, hipStream_t st) {
   constexpr int NT = 64 * WM * WN;
-  if (prec == 0) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, KM, 0>), grid, dim3(NT), 0, st, kp);
-  else if (prec == 1) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, KM, 1>), grid, dim3(NT), 0, st, kp);
-  else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, KM, 2>), grid, dim3(NT), 0, st, kp);
+  if (prec == 0) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, KM, 0, PRO>), grid, dim3(NT), 0, st, kp);
+  else if (prec == 1) hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, KM, 1, PRO>), grid, dim3(NT), 0, st, kp);
+  else hipLaunchKernelGGL((conv_igemm_kernel<BM, BN, WM, WN, KM, 2, PRO>), grid, dim3(NT), 0, st, kp);
   return launch_status();
 }
 
@@ -508,9 +539,12 @@ int launch_cfg(const ConvK& kp0, int km, int prec, hipStream_t st) {
   kp.tiles_n = (kp.Co + BN - 1) / BN;
   kp.nwg = tiles_m * kp.tiles_n;
   dim3 grid(kp.nwg);
-  if (km == 2) return launch_km<BM, BN, WM, WN, 2>(kp, prec, grid, st);
-  if (km == 1) return launch_km<BM, BN, WM, WN, 1>(kp, prec, grid, st);
-  if constexpr ((64 * WM * WN) % BM == 0) return launch_km<BM, BN, WM, WN, 0>(kp, prec, grid, st);
+  const bool pro = kp.in_scale != nullptr;
+  if (km == 2) return pro ? launch_km<BM, BN, WM, WN, 2, true>(kp, prec, grid, st)
+                          : launch_km<BM, BN, WM, WN, 2, false>(kp, prec, grid, st);
+  if (km == 1) return pro ? launch_km<BM, BN, WM, WN, 1, true>(kp, prec, grid, st)
+                          : launch_km<BM, BN, WM, WN, 1, false>(kp, prec, grid, st);
+  if constexpr ((64 * WM * WN) % BM == 0) return launch_km<BM, BN, WM, WN, 0, false>(kp, prec, grid, st);
   return PRPE_EINVAL;
 }
 
@@ -542,8 +576,10 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   if (d->k_order == 1 && (!vec || x.c % 32 != 0)) return PRPE_EINVAL;
   const int km = d->k_order == 1 ? 2 : (vec ? 1 : 0);
   if (km == 0 && d->k_pad > 1024) return PRPE_EINVAL;
-  // the input-side affine is implemented on the vector paths only (IR-50 pre-BN, Ci >= 64)
+  // the input-side affine is implemented on the vector paths only (IR-50 pre-BN, Ci >= 64);
+  // the vector paths keep one validity bit per kh and per kw
   if (km == 0 && d->in_scale) return PRPE_EINVAL;
+  if (km != 0 && (d->kh > 32 || d->kw > 32)) return PRPE_EINVAL;
 
   ConvK kp{};
   kp.x = x.ptr; kp.xsn = x.sn; kp.xsh = x.sh; kp.xsw = x.sw; kp.xsc = x.sc;

@@ -138,16 +138,17 @@ class Engine:
         return ops.upconv3x3(z, out, align_corners, self._aux[key], self._aux[key + "b"], slope, act)
 
     # ------------------------------------------------------------------ ResNet-50 trunk
-    def trunk(self, x_nchw):
-        """MultiTaskResNetFeatureExtractor (modify_models.py:427-437), torchvision v1.5."""
+    def trunk(self, x_nchw, flip_w=False):
+        """MultiTaskResNetFeatureExtractor (modify_models.py:427-437), torchvision v1.5.
+        ``flip_w``: run on the W-mirrored frames (torch.flip(images, dims=[-1]))."""
         with self.prec("trunk"):
-            return self._trunk(x_nchw)
+            return self._trunk(x_nchw, flip_w)
 
-    def _trunk(self, x_nchw):
+    def _trunk(self, x_nchw, flip_w=False):
         # NCHW frames -> NHWC4 (zero 4th channel) so the 7x7/2 stem runs the vectorised
         # implicit-GEMM path; its weight gets a matching zero input channel
         B0, _, H0, W0 = x_nchw.shape
-        x = ops.copy_pad(ops.nhwc(x_nchw), self.empty(B0, H0, W0, 4))
+        x = ops.copy_pad(ops.nhwc(x_nchw), self.empty(B0, H0, W0, 4), flip_w=flip_w)
         stem = self._packs.get("backbone.conv1")
         if stem is None:
             w = self.sd["backbone.conv1.weight"].float()

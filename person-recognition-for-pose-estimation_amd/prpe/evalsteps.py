@@ -1,0 +1,86 @@
+"""Device halves of the reference eval steps that wrap the model.
+
+* ``pose_flip_test``  — PoseEstimationModule.validation_step's flip test
+  (training/lightning/pose_estimation/module.py:466-484): heatmaps of the frames and of the
+  W-mirrored frames (the mirror is a negative-stride read in the stem's layout kernel, no
+  flipped copy), flipped back and averaged by one kernel (prpe_flip_average). ``mode``:
+  "reference" reproduces ``flipped[:, pair] = flipped[:, pair].flip(0)`` literally (that
+  reverses the BATCH order of the paired channels); "swap" exchanges the pair's channels.
+* ``FaceRecognitionEval`` — FaceRecognitionModule.validation_step's head
+  (training/lightning/face_recognition/module.py:133-145): F.normalize of the [512, classes]
+  head kernel (rows, dim=1) once per kernel, then per batch F.normalize(embeddings), the
+  [B,512] x [512,classes] cosine GEMM with the scale s folded into the epilogue (prpe_conv2d,
+  fp32-faithful 3-plane mode), and cross-entropy + argmax + accuracy on device
+  (prpe_ce_argmax).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+from .pack import pack_matrix
+
+COCO_FLIP_PAIRS = [(1, 2), (3, 4), (5, 6), (7, 8), (9, 10), (11, 12), (13, 14), (15, 16)]  # datamodule.py:25-34
+
+
+def flip_partner(k: int = 17, pairs=COCO_FLIP_PAIRS) -> list[int]:
+    part = [-1] * k
+    for a, b in pairs:
+        part[a], part[b] = b, a
+    return part
+
+
+@torch.no_grad()
+def pose_flip_test(model, images, mode: str = "reference"):
+    """Averaged flip-test heatmaps [B,17,64,48] for ``images`` [B,3,H,W] (module.py:466-484)."""
+    if mode not in ("reference", "swap"):
+        raise ValueError(f"unknown flip mode {mode!r}")
+    e = model.engine
+    x = model._check_input(images)
+    heat = e.vitpose(e.trunk(x))
+    heat_f = e.vitpose(e.trunk(x, flip_w=True))
+    return ops.flip_average(heat, heat_f, flip_partner(heat.shape[1]), 0 if mode == "reference" else 1)
+
+
+class FaceRecognitionEval:
+    """(loss, acc) of the face-recognition eval step, on device."""
+
+    def __init__(self, model, s: float = 64.0, precision: int = 2):
+        kernel = model.ada_face.head.kernel
+        if kernel is None:
+            raise ValueError("model.ada_face.head.kernel is not set (load a state_dict that has it)")
+        self.model = model
+        self.s = float(s)
+        self.precision = precision
+        self.set_kernel(kernel)
+
+    def set_kernel(self, kernel):
+        """Normalise + pack the [512, classes] head kernel (call again after it changes)."""
+        k = kernel.to(self.model.device, torch.float32).contiguous()
+        d, ncls = k.shape
+        kn = torch.empty_like(k)
+        ops.l2norm(k, kn, torch.empty(d, device=k.device))            # F.normalize(kernel), dim=1
+        self.classes = ncls
+        self.pack = pack_matrix("ada_face.head:logits", kn.t().cpu(), 1, 1, d, 1, 0, self.model.device,
+                                scale=torch.full((ncls,), self.s))
+
+    def logits(self, embeddings):
+        B, d = embeddings.shape
+        e = embeddings.contiguous().float()
+        en = torch.empty_like(e)
+        ops.l2norm(e, en, torch.empty(B, device=e.device))            # F.normalize(embeddings)
+        out = torch.empty(B, 1, 1, self.classes, device=e.device)
+        ops.conv2d(en.view(B, 1, 1, d), self.pack, out, precision=self.precision)
+        return out.view(B, self.classes)
+
+    @torch.no_grad()
+    def __call__(self, images=None, labels=None, embeddings=None):
+        """Returns (loss, acc, argmax) as device tensors; pass ``embeddings`` to skip the model."""
+        if embeddings is None:
+            self.model.set_task("face_recognition")
+            embeddings, _ = self.model(images)
+        out = self.logits(embeddings)
+        loss, amax, summary = ops.ce_argmax(out, labels)
+        if labels is None:
+            return None, None, amax
+        return summary[0], summary[1], amax

@@ -79,8 +79,14 @@ def maxpool(x, y, k, stride, pad):
     return y
 
 
-def copy_pad(x, y):
-    check(lib().prpe_copy_pad(C.byref(view(x)), C.byref(view(y)), _stream()), "prpe_copy_pad")
+def copy_pad(x, y, flip_w=False):
+    """y = x zero-padded in C; ``flip_w`` reads x mirrored along W (a negative-stride view,
+    so the flip-test pass needs no flipped copy of the frames)."""
+    xv = view(x)
+    if flip_w:
+        xv.ptr = x.data_ptr() + (x.shape[2] - 1) * x.stride(2) * x.element_size()
+        xv.sw = -x.stride(2)
+    check(lib().prpe_copy_pad(C.byref(xv), C.byref(view(y)), _stream()), "prpe_copy_pad")
     return y
 
 
@@ -153,3 +159,29 @@ def softargmax(heat, boxes=None, want_argmax=False):
     check(lib().prpe_softargmax(heat.data_ptr(), B, K, H, W, _ptr(bx), coords.data_ptr(), scores.data_ptr(),
                                 _ptr(am), _stream()), "prpe_softargmax")
     return (coords, scores, am) if want_argmax else (coords, scores)
+
+
+def flip_average(heat, heat_flipped, partner, mode=0):
+    """Pose flip test: (heat + flipback(heat_flipped)) * 0.5 (pose_estimation/module.py:470-484)."""
+    heat, heat_flipped = heat.contiguous(), heat_flipped.contiguous()
+    B, K, H, W = heat.shape
+    out = torch.empty_like(heat)
+    pa = (C.c_int32 * K)(*[int(v) for v in partner])
+    check(lib().prpe_flip_average(heat.data_ptr(), heat_flipped.data_ptr(), out.data_ptr(), B, K, H, W, pa, mode,
+                                  _stream()), "prpe_flip_average")
+    return out
+
+
+def ce_argmax(logits, labels=None):
+    """Per-row argmax (+ cross-entropy and the [mean loss, acc] summary when labels given)."""
+    B, Cn = logits.shape
+    assert logits.stride(1) == 1
+    amax = torch.empty(B, device=logits.device, dtype=torch.int32)
+    loss = summary = None
+    if labels is not None:
+        labels = labels.to(device=logits.device, dtype=torch.int64).contiguous()
+        loss = torch.empty(B, device=logits.device, dtype=torch.float32)
+        summary = torch.empty(2, device=logits.device, dtype=torch.float32)
+    check(lib().prpe_ce_argmax(logits.data_ptr(), logits.stride(0), B, Cn, _ptr(labels), _ptr(loss), amax.data_ptr(),
+                               _ptr(summary), _stream()), "prpe_ce_argmax")
+    return loss, amax, summary
