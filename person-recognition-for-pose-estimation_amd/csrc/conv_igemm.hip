@@ -33,6 +33,10 @@ namespace {
 
 constexpr int BK = 32;
 
+// 16 zero bytes: the gather source of out-of-bounds taps (padding), so a loaded value never
+// needs a select afterwards
+__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
+
 struct ConvK {
   const float* x; int64_t xsn, xsh, xsw, xsc; int Hi, Wi, Ci;
   float* y; int64_t ysn, ysh, ysw, ysc; int Ho, Wo, Co;
@@ -62,7 +66,7 @@ typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 // (one bit per kh and per kw) are computed once, the K-step offset is wave-uniform (KM 2) or
 // advanced incrementally (KM 1).
 template <int BM, int BN, int WM, int WN, int KM, int PREC, bool PRO>
-__global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
+__global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
   constexpr int NT = 64 * WM * WN;
   constexpr bool VEC = KM != 0;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -198,15 +202,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
         c_off += BK;
         c_advance();
       }
-      // Branch-free gather: out-of-bounds rows load element 0 and are zeroed in store_tile
-      // through amask. Nothing here consumes a loaded value, so the loads stay in flight
-      // across compute().
+      // Branch-free gather: out-of-bounds taps read 16 zero bytes (PRO: their affine result is
+      // zeroed in store_tile through amask). Nothing here consumes a loaded value, so the
+      // loads stay in flight across compute().
       amask = 0;
 #pragma unroll
       for (int i = 0; i < A_ROWS_PT; ++i) {
         const bool ok = kval && ((hmask[i] >> kh) & (wmask[i] >> kw) & 1u);
-        areg[i] = *reinterpret_cast<const f4*>(p.x + (ok ? rbase[i] + off : 0));
-        amask |= (unsigned)ok << i;
+        const float* src = ok ? p.x + (rbase[i] + off) : g_zero4;
+        areg[i] = *reinterpret_cast<const f4*>(src);
+        if constexpr (PRO) amask |= (unsigned)ok << i;
       }
     } else {
       const int kk0 = tid / BM;
@@ -237,18 +242,24 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
     }
   };
 
-  auto store_tile = [&](int buf) {
+  // The staging writes of the next tile are split into pieces (one A row each, then B) that
+  // compute() interleaves with its MFMA rows, so the split/convert VALU work and the LDS
+  // writes issue under the MFMAs instead of after them.
+  constexpr int NPIECE = VEC ? A_ROWS_PT + 1 : 1;
+  auto store_piece = [&](int buf, int piece) {
     if constexpr (VEC) {
       const int c4 = tid & 7;
-#pragma unroll
-      for (int i = 0; i < A_ROWS_PT; ++i) {
+      if (piece < A_ROWS_PT) {
+        const int i = piece;
         const int row = (tid >> 3) + RPASS * i;
         const int slot = (c4 >> 1) ^ swzF(row);
         const int off = row * BK + slot * 8 + (c4 & 1) * 4;
         bf16x4 pl[NP];
         f4 v = areg[i];
-        if constexpr (PRO) v = v * as4 + ab4;
-        if (!((amask >> i) & 1u)) v = f4{0.f, 0.f, 0.f, 0.f};   // padding stays 0 (no prologue)
+        if constexpr (PRO) {
+          v = v * as4 + ab4;
+          if (!((amask >> i) & 1u)) v = f4{0.f, 0.f, 0.f, 0.f};   // padding stays 0 (no prologue)
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           float r = v[e];
@@ -261,6 +272,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
         }
 #pragma unroll
         for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x4*>(A_at(buf, q) + off) = pl[q];
+        return;
       }
     } else {
       const int row = tid % BM, kk0 = tid / BM;
@@ -290,6 +302,10 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
       }
     }
   };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int pc = 0; pc < NPIECE; ++pc) store_piece(buf, pc);
+  };
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -299,7 +315,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
 
   const int fr = lane & 15, fg = lane >> 4;
 
-  auto compute = [&](int buf) {
+  auto compute = [&](int buf, int nbuf, bool stage) {
     bf16x8 af[NP][TM], bfr[NP][TN];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -317,7 +333,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
     }
     // partial products smallest first; terms with plane-index sum >= NP are dropped
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
 #pragma unroll
@@ -326,6 +342,14 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
           for (int qa = s; qa >= 0; --qa)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[qa][i], bfr[s - qa][j], acc[i][j], 0, 0, 0);
       }
+      // pieces go behind the second half of the MFMA rows: the global loads they consume
+      // were issued at the top of this K-step and need that long to land
+      constexpr int H0 = TM / 2, NR = TM - H0;
+      if (stage && i >= H0) {
+#pragma unroll
+        for (int pc = (i - H0) * NPIECE / NR; pc < (i - H0 + 1) * NPIECE / NR; ++pc) store_piece(nbuf, pc);
+      }
+    }
   };
 
   // ---------------- main loop
@@ -334,9 +358,9 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_igemm_kernel(ConvK p) {
   __syncthreads();
   for (int kt = 0; kt < p.nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < p.nk) load_tile(kt + 1);
-    compute(cur);
-    if (kt + 1 < p.nk) store_tile(cur ^ 1);
+    const bool more = kt + 1 < p.nk;
+    if (more) load_tile(kt + 1);
+    compute(cur, cur ^ 1, more);
     __syncthreads();
   }
 
@@ -623,7 +647,7 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   // the 2-plane mode is near-flat between 128x128 and 256x128 (256x128 +2% on 3x3) and
   // prefers 256x64 for Co <= 64
   if (tile == 0) {
-    if (y.c > 64) tile = (prec == 2 || khw > 1) ? 5 : 1;
+    if (y.c > 64) tile = (prec == 2 || khw > 1) ? 5 : (x.c <= 128 ? 6 : 1);
     else if (y.c > 32) tile = prec == 2 ? 2 : 6;
     else tile = y.c > 16 ? 3 : 4;
   }
