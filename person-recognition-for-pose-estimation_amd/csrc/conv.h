@@ -1,0 +1,63 @@
+// Shared definitions of the two implicit-GEMM conv kernels (conv_igemm.hip: register-staged,
+// any layout; conv_glds.hip: direct global->LDS staging for channel-chunked inputs).
+#pragma once
+#include "common.h"
+
+namespace prpe_k {
+
+// Kernel arguments of prpe_conv2d (host-validated, see conv_igemm.hip)
+struct ConvK {
+  const float* x; int64_t xsn, xsh, xsw, xsc; int Hi, Wi, Ci;
+  float* y; int64_t ysn, ysh, ysw, ysc; int Ho, Wo, Co;
+  const float* r; int64_t rsn, rsh, rsw, rsc;
+  int KH, KW, stride, pad, K, k_pad, nk;
+  const uint16_t* whi; const uint16_t* wlo; const uint16_t* wlo2;
+  const float* scale; const float* bias; const float* slope;
+  const float* in_scale; const float* in_bias;
+  int act, res_mode, vec_out;
+  int M, HoWo, tiles_n, nwg;
+  const float* zero;   // &g_zero4 on this device (a kernel argument, so the K-loop does not
+                       // re-load the symbol's address from the GOT every step)
+};
+
+// F = {0,2,3,1} indexed by (row >> 2) & 3, branch-free
+__device__ __forceinline__ int swzF(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
+
+// native vector types: HIP's float4/uint4 are structs, and arrays of them cannot be promoted
+// to registers (the compiler moved them to a per-thread LDS array with 64-B lane stride)
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+
+// fp32 x4 -> NP bf16 planes, two lanes at a time: hi = RNE(v) (v_cvt_pk_bf16_f32), its fp32
+// value rebuilt by a shift / mask, remainder by one packed subtract, and so on per plane
+// (the compiler's per-element lowering of the same casts took 13 VALU per float4 at NP 2)
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+template <int NP>
+__device__ __forceinline__ void split_planes(f4 v, bf16x4 (&pl)[NP]) {
+  f2v r[2] = {f2v{v[0], v[1]}, f2v{v[2], v[3]}};
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    unsigned u[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bf16x2v b = __builtin_convertvector(r[h], bf16x2v);
+      u[h] = __builtin_bit_cast(unsigned, b);
+      if (q + 1 < NP) {
+        const f2v back = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
+        r[h] = r[h] - back;
+      }
+    }
+    pl[q] = __builtin_bit_cast(bf16x4, (unsigned long long)u[0] | ((unsigned long long)u[1] << 32));
+  }
+}
+
+
+
+// direct global->LDS kernel (conv_glds.hip): Ci % 32 == 0 channel-contiguous input, chunk-major
+// weights, precision 0 or 2, no prologue; tile 0 = auto, 10..12 = 256x128 / 256x64 / 128x128.
+// Returns PRPE_EINVAL when the shape is not eligible.
+bool conv_glds_eligible(const ConvK& kp, int prec, int km);
+int conv_glds_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
+
+}  // namespace prpe_k

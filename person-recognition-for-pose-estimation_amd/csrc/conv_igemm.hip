@@ -27,7 +27,8 @@
 //
 // Reference arithmetic replaced: torch Conv2d (+BatchNorm2d eval +act +residual) at every
 // call site listed in include/prpe.h (prpe_conv2d).
-#include "common.h"
+#include "conv.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -37,25 +38,7 @@ constexpr int BK = 32;
 // needs a select afterwards
 __device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
 
-struct ConvK {
-  const float* x; int64_t xsn, xsh, xsw, xsc; int Hi, Wi, Ci;
-  float* y; int64_t ysn, ysh, ysw, ysc; int Ho, Wo, Co;
-  const float* r; int64_t rsn, rsh, rsw, rsc;
-  int KH, KW, stride, pad, K, k_pad, nk;
-  const uint16_t* whi; const uint16_t* wlo; const uint16_t* wlo2;
-  const float* scale; const float* bias; const float* slope;
-  const float* in_scale; const float* in_bias;
-  int act, res_mode, vec_out;
-  int M, HoWo, tiles_n, nwg;
-};
-
-// F = {0,2,3,1} indexed by (row >> 2) & 3, branch-free
-__device__ __forceinline__ int swzF(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
-
-// native vector types: HIP's float4/uint4 are structs, and arrays of them cannot be promoted
-// to registers (the compiler moved them to a per-thread LDS array with 64-B lane stride)
-typedef float f4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+using namespace prpe_k;
 
 // KM: 0 = scalar gather through a k -> (kh,kw,ci) LUT (any Ci, e.g. 3-channel inputs)
 //     1 = vector loads, tap-major K (Ci % 4 == 0)
@@ -209,7 +192,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
 #pragma unroll
       for (int i = 0; i < A_ROWS_PT; ++i) {
         const bool ok = kval && ((hmask[i] >> kh) & (wmask[i] >> kw) & 1u);
-        const float* src = ok ? p.x + (rbase[i] + off) : g_zero4;
+        const float* src = ok ? p.x + (rbase[i] + off) : p.zero;
         areg[i] = *reinterpret_cast<const f4*>(src);
         if constexpr (PRO) amask |= (unsigned)ok << i;
       }
@@ -260,16 +243,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
           v = v * as4 + ab4;
           if (!((amask >> i) & 1u)) v = f4{0.f, 0.f, 0.f, 0.f};   // padding stays 0 (no prologue)
         }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float r = v[e];
-#pragma unroll
-          for (int q = 0; q < NP; ++q) {
-            const __bf16 t = (__bf16)r;
-            pl[q][e] = t;
-            r -= (float)t;
-          }
-        }
+        split_planes<NP>(v, pl);
 #pragma unroll
         for (int q = 0; q < NP; ++q) *reinterpret_cast<bf16x4*>(A_at(buf, q) + off) = pl[q];
         return;
@@ -625,6 +599,18 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   kp.vec_out = a16(y) && (d->res_mode == PRPE_RES_NONE || a16(d->res)) &&
                (!d->scale || (uintptr_t)d->scale % 16 == 0) && (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
                (!d->slope || (uintptr_t)d->slope % 16 == 0);
+  {
+    // per-device address of the zero page (one host query per device, then cached)
+    static const float* zero_by_dev[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return PRPE_EINVAL;
+    if (!zero_by_dev[dev]) {
+      void* zp = nullptr;
+      if (hipGetSymbolAddress(&zp, HIP_SYMBOL(g_zero4)) != hipSuccess || !zp) return PRPE_EINVAL;
+      zero_by_dev[dev] = static_cast<const float*>(zp);
+    }
+    kp.zero = zero_by_dev[dev];
+  }
   hipStream_t st = as_stream(stream);
   const int prec = d->precision;
   int tile = d->tile;
@@ -642,6 +628,15 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     else hipLaunchKernelGGL((conv_smallco_kernel<4, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
     return launch_status();
   }
+  // direct global->LDS kernel (conv_glds.hip) for chunked inputs with Co > 32; tile 10..12
+  // forces one of its tiles. PRPE_CONV_GLDS=0 in the environment keeps every conv on this
+  // file's register-staged kernel (A/B measurements).
+  static const int glds_on = [] {
+    const char* e = getenv("PRPE_CONV_GLDS");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  if (tile >= 10) return conv_glds_eligible(kp, prec, km) ? conv_glds_launch(kp, prec, tile, st) : PRPE_EINVAL;
+  if (tile == 0 && glds_on && y.c > 32 && conv_glds_eligible(kp, prec, km)) return conv_glds_launch(kp, prec, 0, st);
   // measured (tools/conv_bench.py, profiles/r01_conv_bench_tiles.txt): the 3-plane mode wants the
   // 256x128 8-wave tile for wide Co (operand traffic per MFMA halves; +30%), 128x64 below;
   // the 2-plane mode is near-flat between 128x128 and 256x128 (256x128 +2% on 3x3) and

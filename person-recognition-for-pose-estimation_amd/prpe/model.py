@@ -114,15 +114,37 @@ class CombinedModel:
     __call__ = forward
 
     @torch.no_grad()
-    def forward_all(self, x, face_stride=None):
-        """Trunk once -> face-YOLO det, AdaFace (emb, norm), ViTPose heatmaps."""
+    def forward_all(self, x, face_stride=None, concurrent=True):
+        """Trunk once -> face-YOLO det, AdaFace (emb, norm), ViTPose heatmaps.
+
+        ``concurrent``: the three heads only share the trunk features, so they are enqueued on
+        three HIP streams (forked from / joined back into the caller's stream by events). The
+        heads' HBM-bound kernels (upsample-conv, pointwise) then co-reside on the CUs with the
+        other heads' MFMA-bound convs, and one kernel's tail wave no longer idles the chip.
+        Same kernels, same arithmetic: results are bit-identical to the sequential order."""
         x = self._check_input(x)
         e = self.engine
         feat = e.trunk(x)
         stride = face_stride if face_stride is not None else self._stride(self.yolo_face)
-        det = e.yolo("yolo_face", feat, stride)
-        emb, norm = e.adaface(feat)
-        heat = e.vitpose(feat)
+        heads = (lambda: e.yolo("yolo_face", feat, stride), lambda: e.adaface(feat), lambda: e.vitpose(feat))
+        if not concurrent:
+            det, (emb, norm), heat = (h() for h in heads)
+            return {"det": det, "emb": emb, "norm": norm, "heatmaps": heat}
+        main = torch.cuda.current_stream(feat.device)
+        if getattr(self, "_head_streams", None) is None or self._head_streams[0].device != feat.device:
+            self._head_streams = [torch.cuda.Stream(feat.device) for _ in heads]
+        fork = main.record_event()
+        outs = []
+        for s, h in zip(self._head_streams, heads):
+            s.wait_event(fork)
+            feat.record_stream(s)            # feat is freed on `main`; keep it alive for `s`
+            with torch.cuda.stream(s):
+                outs.append(h())
+        for s in self._head_streams:
+            main.wait_stream(s)
+        det, (emb, norm), heat = outs
+        for t in (det, emb, norm, heat):
+            t.record_stream(main)            # allocated on a head stream, consumed on `main`
         return {"det": det, "emb": emb, "norm": norm, "heatmaps": heat}
 
     @staticmethod

@@ -87,6 +87,14 @@ def test_forward_all_matches_per_task(model, frames, golden_model):
     np.testing.assert_allclose(o["det"].cpu().numpy()[:, 4], golden_model["det_face_s8"][:, 4], atol=1e-3)
 
 
+def test_forward_all_concurrent_heads_bit_identical(model, frames):
+    # the three heads on their own streams run the same kernels as the sequential order
+    a = model.forward_all(frames, face_stride=[8.0, 16.0, 32.0], concurrent=True)
+    b = model.forward_all(frames, face_stride=[8.0, 16.0, 32.0], concurrent=False)
+    for k in ("det", "emb", "norm", "heatmaps"):
+        assert torch.equal(a[k], b[k]), k
+
+
 def test_nms_on_model_output_bit_exact_vs_oracle(model, frames, golden_model):
     o = model.forward_all(frames, face_stride=[8.0, 16.0, 32.0])
     det = o["det"]

@@ -27,14 +27,14 @@ def main():
     e = m.engine
     e.prepare()
     x = synth.frames(a.batch).cuda()
-    m.forward_all(x, face_stride=[8.0, 16.0, 32.0])
+    m.forward_all(x, face_stride=[8.0, 16.0, 32.0], concurrent=False)
     torch.cuda.synchronize()
     e.watch = set(e._packs.keys())
     e.events = {}
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     t0.record()
-    m.forward_all(x, face_stride=[8.0, 16.0, 32.0])
+    m.forward_all(x, face_stride=[8.0, 16.0, 32.0], concurrent=False)
     t1.record()
     torch.cuda.synchronize()
     total = t0.elapsed_time(t1)

@@ -1,19 +1,49 @@
 """Diagnostics (GPU box): parity vs the reference's golden outputs under several conv
-precision policies (bs=2, 640x640)."""
-import os, sys
+precision policies (bs=2, 640x640), plus the forward time of each policy at bs=64.
+
+precision per component: 2 = 3-plane split (fp32-faithful operands, 6 MFMA terms),
+0 = 2-plane split (3 terms, ~2^-17 per product), 1 = plain bf16 (1 term, diagnostics)."""
+import os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "person-recognition-for-pose-estimation_amd")]
 import numpy as np, torch
 from prpe import CombinedModel, arch, synth
+from prpe.postproc import keypoints_from_heatmaps, non_max_suppression
+from oracle import model_ref as R
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from test_gpu_model import nms_match_rate
 
 g = dict(np.load(os.path.join(ROOT, "tests/golden/golden_model.npz")))
 sd = synth.make_state_dict(arch.state_dict_spec())
 x = synth.frames(2).cuda()
-for name, pol in [("auto", "auto"), ("yolo_net=0", {"yolo_net": 0}), ("yolo all 2", {"yolo_adapter": 2}),
-                  ("all 2", 2), ("all 0", 0)]:
+xb = synth.frames(64).cuda()
+ref_nms = R.non_max_suppression(torch.from_numpy(g["det_face_s8"]))
+cr, _ = R.keypoints_from_heatmaps(torch.from_numpy(g["heatmaps"]))
+POL = [("auto", "auto"), ("trunk=0", {"trunk": 0}), ("yolo_net=0", {"yolo_net": 0}),
+       ("all 0", 0), ("all 2", 2), ("vit=1", {"vit": 1}), ("adaface=1", {"adaface": 1}),
+       ("yolo_ad=1", {"yolo_adapter": 1}), ("trunk=1", {"trunk": 1})]
+sel = sys.argv[1:]
+for name, pol in POL:
+    if sel and name not in sel:
+        continue
     m = CombinedModel(sd, precision=pol)
     o = m.forward_all(x, face_stride=[8.0, 16.0, 32.0])
-    d = o["det"].cpu().numpy(); r = g["det_face_s8"]
-    print(f"{name:12s} cls {np.abs(d[:,4]-r[:,4]).max():.2e} box {np.abs(d[:,:4]-r[:,:4]).max():.2e} "
+    d = o["det"].cpu()
+    r = g["det_face_s8"]
+    rates = [nms_match_rate(a.cpu(), b) for a, b in zip(non_max_suppression(o["det"]), ref_nms)]
+    c, _ = keypoints_from_heatmaps(o["heatmaps"])
+    oks = R.oks_delta(c.cpu(), cr)
+    m.forward_all(xb, face_stride=[8.0, 16.0, 32.0])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(3):
+        m.forward_all(xb, face_stride=[8.0, 16.0, 32.0])
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / 3 * 1e3
+    dn = d.numpy()
+    print(f"{name:11s} cls {np.abs(dn[:,4]-r[:,4]).max():.2e} box {np.abs(dn[:,:4]-r[:,:4]).max():.2e} "
           f"heat {np.abs(o['heatmaps'].cpu().numpy()-g['heatmaps']).max():.2e} "
-          f"emb {np.abs(o['emb'].cpu().numpy()-g['emb']).max():.2e}", flush=True)
+          f"emb {np.abs(o['emb'].cpu().numpy()-g['emb']).max():.2e} oks {oks:.1e} "
+          f"nms_match {min(rates):.3f}  bs64 {ms:.1f} ms", flush=True)
+    del m
+    torch.cuda.empty_cache()
