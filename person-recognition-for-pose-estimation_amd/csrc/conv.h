@@ -16,8 +16,10 @@ struct ConvK {
   const float* in_scale; const float* in_bias;
   int act, res_mode, vec_out;
   int M, HoWo, tiles_n, nwg;
-  const float* zero;   // &g_zero4 on this device (a kernel argument, so the K-loop does not
-                       // re-load the symbol's address from the GOT every step)
+  const float* zero;   // &g_zero8 on this device (a kernel argument, so the K-loop does not
+                       // re-load the symbol's address from the GOT every step); 32 zero bytes
+  int ylin, rlin;      // y (r) offset of pixel m is m * ysw (rsw): contiguous pixels, so the
+                       // epilogue skips the m -> (n, oh, ow) division
 };
 
 // F = {0,2,3,1} indexed by (row >> 2) & 3, branch-free
@@ -54,10 +56,32 @@ __device__ __forceinline__ void split_planes(f4 v, bf16x4 (&pl)[NP]) {
 
 
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) void* gbl_ptr_t;
+
+// one LDS-DMA piece: 16 B per lane from src (per lane) to dst_lds + 16 * lane (dst wave-uniform)
+__device__ __forceinline__ void glds16(const void* src, void* dst_lds) {
+  __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src), (lds_ptr_t)(dst_lds), 16, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) + s_barrier in one asm statement with a memory clobber: no LDS access
+// may be moved across it, and it does not drain the LDS-DMA copies still in flight (a
+// __syncthreads() would emit vmcnt(0) here)
+template <int N>
+__device__ __forceinline__ void wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
 // direct global->LDS kernel (conv_glds.hip): Ci % 32 == 0 channel-contiguous input, chunk-major
 // weights, precision 0 or 2, no prologue; tile 0 = auto, 10..12 = 256x128 / 256x64 / 128x128.
 // Returns PRPE_EINVAL when the shape is not eligible.
 bool conv_glds_eligible(const ConvK& kp, int prec, int km);
 int conv_glds_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
+
+// wave-row kernel (conv_wave.hip): A straight into MFMA fragment registers, B planes through
+// an LDS-DMA ring; chunked inputs, precision 0 / 2, optional prologue affine; tile 20 = auto,
+// 21..25 force a configuration.
+bool conv_wave_eligible(const ConvK& kp, int prec, int km);
+int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 
 }  // namespace prpe_k

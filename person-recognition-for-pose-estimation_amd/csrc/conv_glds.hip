@@ -17,7 +17,7 @@
 // LDS images are lane-linear (a glds writes base + 16*lane), so the XOR swizzles that make the
 // fragment reads conflict-free are applied to the per-lane SOURCE address (and undone on the
 // read): A slot c of row r sits at physical slot c ^ ((r >> 1) & 7) in its 128-B row; B chunk j
-// of row n at j ^ swzF(n) in its 64-B row. Padding taps read a 16-B zero page.
+// of row n at j ^ swzF(n) in its 64-B row. Padding taps read a zero page.
 #include "conv.h"
 
 namespace prpe_k {
@@ -26,21 +26,6 @@ namespace {
 constexpr int BK = 32;
 
 __device__ __forceinline__ int swzA(int r) { return (r >> 1) & 7; }
-
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
-typedef __attribute__((address_space(1))) void* gbl_ptr_t;
-
-__device__ __forceinline__ void glds16(const void* src, void* dst_lds) {
-  __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src), (lds_ptr_t)(dst_lds), 16, 0, 0);
-}
-
-// s_waitcnt vmcnt(N) + s_barrier in one asm statement with a memory clobber: no LDS access
-// may be moved across it, and it does not drain the glds copies still in flight (a
-// __syncthreads() would emit vmcnt(0) here)
-template <int N>
-__device__ __forceinline__ void wait_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
-}
 
 template <int BM, int BN, int NW, int NP, int STAGES>
 __global__ __launch_bounds__(NW * 64, 2) void conv_glds_kernel(ConvK p) {

@@ -34,9 +34,9 @@ namespace {
 
 constexpr int BK = 32;
 
-// 16 zero bytes: the gather source of out-of-bounds taps (padding), so a loaded value never
-// needs a select afterwards
-__device__ __attribute__((aligned(16))) float g_zero4[4] = {0.f, 0.f, 0.f, 0.f};
+// 32 zero bytes: the gather source of out-of-bounds taps (padding), so a loaded value never
+// needs a select afterwards (conv_wave reads 32 B per lane and row)
+__device__ __attribute__((aligned(32))) float g_zero8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 
 using namespace prpe_k;
 
@@ -599,6 +599,9 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   kp.vec_out = a16(y) && (d->res_mode == PRPE_RES_NONE || a16(d->res)) &&
                (!d->scale || (uintptr_t)d->scale % 16 == 0) && (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
                (!d->slope || (uintptr_t)d->slope % 16 == 0);
+  kp.ylin = y.sh == (int64_t)Wo * y.sw && y.sn == (int64_t)Ho * y.sh;
+  kp.rlin = d->res_mode == PRPE_RES_NONE ||
+            (d->res.sh == (int64_t)Wo * d->res.sw && d->res.sn == (int64_t)Ho * d->res.sh);
   {
     // per-device address of the zero page (one host query per device, then cached)
     static const float* zero_by_dev[64] = {};
@@ -606,7 +609,7 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return PRPE_EINVAL;
     if (!zero_by_dev[dev]) {
       void* zp = nullptr;
-      if (hipGetSymbolAddress(&zp, HIP_SYMBOL(g_zero4)) != hipSuccess || !zp) return PRPE_EINVAL;
+      if (hipGetSymbolAddress(&zp, HIP_SYMBOL(g_zero8)) != hipSuccess || !zp) return PRPE_EINVAL;
       zero_by_dev[dev] = static_cast<const float*>(zp);
     }
     kp.zero = zero_by_dev[dev];
@@ -635,7 +638,16 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const char* e = getenv("PRPE_CONV_GLDS");
     return e && e[0] == '0' ? 0 : 1;
   }();
+  static const int wave_on = [] {
+    const char* e = getenv("PRPE_CONV_WAVE");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  if (tile >= 20) return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile, st) : PRPE_EINVAL;
   if (tile >= 10) return conv_glds_eligible(kp, prec, km) ? conv_glds_launch(kp, prec, tile, st) : PRPE_EINVAL;
+  // wave-row kernel everywhere it applies except two-plane Co <= 64, where the LDS-staged
+  // 256x64 tile measured faster (profiles/r01_conv_bench_wave.txt)
+  if (tile == 0 && wave_on && y.c > 32 && (prec == 2 || y.c > 64) && conv_wave_eligible(kp, prec, km))
+    return conv_wave_launch(kp, prec, 20, st);
   if (tile == 0 && glds_on && y.c > 32 && conv_glds_eligible(kp, prec, km)) return conv_glds_launch(kp, prec, 0, st);
   // measured (tools/conv_bench.py, profiles/r01_conv_bench_tiles.txt): the 3-plane mode wants the
   // 256x128 8-wave tile for wide Co (operand traffic per MFMA halves; +30%), 128x64 below;

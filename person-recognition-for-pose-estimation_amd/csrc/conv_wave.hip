@@ -1,0 +1,318 @@
+// Implicit-GEMM convolution on CDNA4 MFMA, "wave-row" variant: every wave owns whole output
+// rows of the block tile (waves tile M only, each wave WTM x BN), the activation operand goes
+// straight from global memory into the wave's MFMA fragment registers, and only the weight
+// planes -- the operand every wave of the block shares -- are staged in LDS.
+//
+// Same GEMM view, K order, split-bf16 arithmetic and MFMA order as conv_igemm.hip / conv_glds.hip
+// (the accumulation order per output element is identical, so the three kernels agree bit for
+// bit):
+//   A[m,k] = PRO(x[n, oh*s-p+kh, ow*s-p+kw, ci]) fp32, B[k,co] = packed bf16 planes [co][k].
+//
+// Why: in the LDS-staged kernels a wave issues 6 LDS-DMA pieces (~60 issue cycles each beside
+// MFMAs), 20 fragment reads and the plane split for 48 MFMAs per K-step, and measured ~40 % of
+// the MFMA rate. Here, at 64x128 per wave and two planes, one K-step is 96 MFMAs against
+// 8 global loads (A, 32 B per lane per row block), 2 LDS-DMA pieces (B), 16 fragment reads and
+// the split of 8 float4 -- the issue budget stays inside the MFMA shadow.
+//
+// A fragment of v_mfma_f32_16x16x32_bf16: lane (fr = lane & 15, fg = lane >> 4) holds row fr,
+// k = 8 fg .. 8 fg + 7 -- i.e. channels 8 fg .. 8 fg + 7 of the K-step's 32-channel chunk at one
+// tap: two 16-B loads. Rows whose tap falls into the padding read a 32-B zero page.
+//
+// Pipeline per K-step kt (B ring STAGES deep, A one step ahead in registers):
+//   wait(my B pieces of step kt) + s_barrier     -- publishes every wave's pieces of step kt
+//   load A(kt+1) -> raw registers                -- in flight across the MFMAs
+//   LDS-DMA B(kt+STAGES-1) into the stage read at kt-1
+//   MFMAs of step kt (B fragments from LDS, A planes in registers)
+//   split raw -> A planes of step kt+1 (waits for A(kt+1), not for the younger B pieces)
+// Loads past the last K-step are clamped to it (a harmless re-read), so the loop body is
+// uniform and the compiler's vmcnt bookkeeping is exact.
+//
+// Epilogue: each wave stages its accumulator rows through a private 16-row LDS slice and
+// writes whole-row 16-B vectors (scale/bias, act, residual), no block barrier.
+#include "conv.h"
+
+namespace prpe_k {
+namespace {
+
+constexpr int BK = 32;
+
+template <int NW, int TM, int TN, int NP, int STAGES, bool PRO>
+__global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
+  constexpr int WTM = TM * 16, BM = NW * WTM, BN = TN * 16;
+  constexpr int B_STAGE = NP * BN * 64;               // bf16 [NP][BN][32]
+  constexpr int NB_TOT = NP * BN / 16;                // 1-KiB LDS-DMA pieces per stage
+  constexpr int IB = (NB_TOT + NW - 1) / NW;          // per wave (surplus slots repeat a piece)
+  constexpr int CS = BN + 4;                          // epilogue row pitch (floats)
+  constexpr int EPI = NW * 16 * CS * 4;
+  constexpr int RING = STAGES * B_STAGE;
+  constexpr int LDS_BYTES = RING > EPI ? RING : EPI;
+  static_assert(STAGES == 2 || STAGES == 3, "stages");
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int L = xcd_remap(blockIdx.x, p.nwg);
+  const int tile_m = L / p.tiles_n, tile_n = L % p.tiles_n;
+  const int n0 = tile_n * BN;
+  const int wrow0 = tile_m * BM + wave * WTM;
+
+  // ---- A rows of this lane: wrow0 + 16 i + fr; element offset of tap (0,0) at channel 8 fg
+  int64_t rbase[TM];
+  unsigned hmask[TM], wmask[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = wrow0 + i * 16 + fr;
+    unsigned hm = 0, wmk = 0;
+    int64_t b = 0;
+    if (m < p.M) {
+      const int n = m / p.HoWo;
+      const int rem = m - n * p.HoWo;
+      const int oh = rem / p.Wo;
+      const int ow = rem - oh * p.Wo;
+      const int ih = oh * p.stride - p.pad, iw = ow * p.stride - p.pad;
+      b = (int64_t)n * p.xsn + (int64_t)ih * p.xsh + (int64_t)iw * p.xsw + fg * 8;
+      for (int t = 0; t < p.KH; ++t) hm |= (unsigned)((unsigned)(ih + t) < (unsigned)p.Hi) << t;
+      for (int t = 0; t < p.KW; ++t) wmk |= (unsigned)((unsigned)(iw + t) < (unsigned)p.Wi) << t;
+    }
+    rbase[i] = b;
+    hmask[i] = hm;
+    wmask[i] = wmk;
+  }
+
+  // ---- B pieces: piece j -> plane j / (BN/16), rows 16 (j % (BN/16)) .. +16; lane -> (row, slot)
+  const uint16_t* bsrc[IB];
+  int bdst[IB];
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    int j = wave * IB + i;
+    if (j >= NB_TOT) j -= NB_TOT;
+    const int q = j / (BN / 16), rb = j % (BN / 16);
+    const int nrow = rb * 16 + (lane >> 2);
+    const int ch = (lane & 3) ^ swzF(nrow);
+    const uint16_t* plane = q == 0 ? p.whi : (q == 1 ? p.wlo : p.wlo2);
+    bsrc[i] = plane + (int64_t)(n0 + nrow) * p.k_pad + ch * 8;
+    bdst[i] = (q * BN + rb * 16) * 64;
+  }
+  auto issue_b = [&](int kt, int stage) {
+    unsigned char* sb = lds + stage * B_STAGE;
+#pragma unroll
+    for (int i = 0; i < IB; ++i) glds16(bsrc[i] + (int64_t)kt * BK, sb + bdst[i]);
+  };
+
+  // ---- A walk (wave-uniform): k = ((ci/32)*KH*KW + kh*KW + kw)*32 + ci%32
+  int u_kh = 0, u_kw = 0, u_ci = 0, u_step = 0;
+  int64_t u_off = 0;                                  // kh*xsh + kw*xsw + chunk*32
+  const int nk = p.nk;
+  f4 raw[TM][2];
+  unsigned amask = 0;
+  f4 as4[2], ab4[2];
+  auto load_a = [&]() {
+    if constexpr (PRO) {
+      as4[0] = *reinterpret_cast<const f4*>(p.in_scale + u_ci + fg * 8);
+      as4[1] = *reinterpret_cast<const f4*>(p.in_scale + u_ci + fg * 8 + 4);
+      ab4[0] = *reinterpret_cast<const f4*>(p.in_bias + u_ci + fg * 8);
+      ab4[1] = *reinterpret_cast<const f4*>(p.in_bias + u_ci + fg * 8 + 4);
+    }
+    amask = 0;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const bool ok = (hmask[i] >> u_kh) & (wmask[i] >> u_kw) & 1u;
+      const float* src = ok ? p.x + (rbase[i] + u_off) : p.zero;
+      raw[i][0] = *reinterpret_cast<const f4*>(src);
+      raw[i][1] = *reinterpret_cast<const f4*>(src + 4);
+      if constexpr (PRO) amask |= (unsigned)ok << i;
+    }
+    // advance to the next K-step (kw, then kh, then the next chunk); stay on the last one
+    if (++u_step < nk) {
+      u_off += p.xsw;
+      if (++u_kw == p.KW) {
+        u_kw = 0; u_off += p.xsh - (int64_t)p.KW * p.xsw;
+        if (++u_kh == p.KH) { u_kh = 0; u_ci += BK; u_off += BK - (int64_t)p.KH * p.xsh; }
+      }
+    } else {
+      u_step = nk - 1;
+    }
+  };
+
+  bf16x8 af[NP][TM];
+  auto split_a = [&]() {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      f4 v0 = raw[i][0], v1 = raw[i][1];
+      if constexpr (PRO) {
+        v0 = v0 * as4[0] + ab4[0];
+        v1 = v1 * as4[1] + ab4[1];
+        if (!((amask >> i) & 1u)) { v0 = f4{0.f, 0.f, 0.f, 0.f}; v1 = v0; }   // padding stays 0
+      }
+      bf16x4 p0[NP], p1[NP];
+      split_planes<NP>(v0, p0);
+      split_planes<NP>(v1, p1);
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+        af[q][i] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int stage) {
+    const unsigned char* sb = lds + stage * B_STAGE;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int nrow = j * 16 + fr;
+      const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
+      bf16x8 bfr[NP];
+#pragma unroll
+      for (int q = 0; q < NP; ++q) bfr[q] = *reinterpret_cast<const bf16x8*>(bp + q * BN * 64);
+      // partial products smallest first; terms with plane-index sum >= NP are dropped
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int s = NP - 1; s >= 0; --s)
+#pragma unroll
+          for (int qa = s; qa >= 0; --qa)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[qa][i], bfr[s - qa], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // ---------------- main loop
+  load_a();
+  issue_b(0, 0);
+  if constexpr (STAGES == 3) issue_b(nk > 1 ? 1 : 0, 1);
+  split_a();
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // B(kt) of this wave: at most the (STAGES-2)*IB pieces issued after it are still pending
+    wait_barrier<(STAGES - 2) * IB>();
+    load_a();
+    {
+      const int ks = kt + STAGES - 1 < nk ? kt + STAGES - 1 : nk - 1;
+      const int sn = st == 0 ? STAGES - 1 : st - 1;   // the stage read at kt-1
+      issue_b(ks, sn);
+    }
+    compute(st);
+    split_a();
+    st = st + 1 == STAGES ? 0 : st + 1;
+  }
+  wait_barrier<0>();   // every LDS-DMA landed and every fragment read retired: LDS is free
+
+  // ---------------- epilogue: per-wave 16-row slices, whole-row 16-B vectors
+  float* ct = reinterpret_cast<float*>(lds) + wave * 16 * CS;
+  constexpr int CPR = BN / 4;                         // float4 chunks per row
+  constexpr int RPP = 64 / CPR;                       // rows per pass
+  constexpr int EB = 16 / RPP;                        // passes per 16-row slice
+  const int cc = lane % CPR, rr0 = lane / CPR;
+  const int col = n0 + cc * 4;
+  const bool cval = col < p.Co;
+  f4 sc4 = {1.f, 1.f, 1.f, 1.f}, bi4 = {0.f, 0.f, 0.f, 0.f}, sl4 = {0.f, 0.f, 0.f, 0.f};
+  if (cval) {
+    if (p.scale) sc4 = *reinterpret_cast<const f4*>(p.scale + col);
+    if (p.bias) bi4 = *reinterpret_cast<const f4*>(p.bias + col);
+    if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
+  }
+  auto offs = [&](int m, int64_t& yo, int64_t& ro) {
+    if (p.ylin && p.rlin) {
+      yo = (int64_t)m * p.ysw + col;
+      ro = (int64_t)m * p.rsw + col;
+      return;
+    }
+    const int n = m / p.HoWo;
+    const int rem = m - n * p.HoWo;
+    const int oh = rem / p.Wo;
+    const int ow = rem - oh * p.Wo;
+    yo = (int64_t)n * p.ysn + (int64_t)oh * p.ysh + (int64_t)ow * p.ysw + col;
+    ro = (int64_t)n * p.rsn + (int64_t)oh * p.rsh + (int64_t)ow * p.rsw + col;
+  };
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) ct[(fg * 4 + r) * CS + j * 16 + fr] = acc[i][j][r];
+    int64_t yo[EB];
+    f4 res[EB];
+    bool ok[EB];
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int m = wrow0 + i * 16 + rr0 + RPP * e;
+      ok[e] = cval && m < p.M;
+      res[e] = f4{0.f, 0.f, 0.f, 0.f};
+      yo[e] = 0;
+      if (ok[e]) {
+        int64_t ro;
+        offs(m, yo[e], ro);
+        if (p.res_mode != PRPE_RES_NONE) res[e] = *reinterpret_cast<const f4*>(p.r + ro);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      f4 v = *reinterpret_cast<const f4*>(ct + (rr0 + RPP * e) * CS + cc * 4);
+      if (!ok[e]) continue;
+      v = v * sc4 + bi4;
+      if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
+      if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
+      *reinterpret_cast<f4*>(p.y + yo[e]) = v;
+    }
+  }
+}
+
+template <int NW, int TM, int TN, int NP, int STAGES>
+int launch(const ConvK& kp0, hipStream_t st) {
+  constexpr int BM = NW * TM * 16, BN = TN * 16;
+  ConvK kp = kp0;
+  const int tiles_m = (kp.M + BM - 1) / BM;
+  kp.tiles_n = (kp.Co + BN - 1) / BN;
+  kp.nwg = tiles_m * kp.tiles_n;
+  if (kp.in_scale)
+    hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  else
+    hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  return launch_status();
+}
+
+}  // namespace
+
+bool conv_wave_eligible(const ConvK& kp, int prec, int km) {
+  // chunk-major K walk (km 2, or any 1x1 on the vector path with whole 32-channel chunks),
+  // vectorised epilogue, precision 0 / 2, K in whole K-steps, B rows readable up to a
+  // multiple of 128
+  const bool chunked = km == 2 || (km == 1 && kp.KH * kp.KW == 1 && kp.Ci % 32 == 0);
+  return chunked && kp.vec_out && (prec == 0 || prec == 2) && kp.K % BK == 0 && kp.k_pad == kp.K &&
+         kp.zero != nullptr;
+}
+
+// tile 20 = auto; 21.. force a configuration (tools/conv_bench.py sweeps them)
+int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
+  if (tile == 20) {
+    // measured (tools/conv_bench.py, profiles/r01_conv_bench_wave.txt): two planes want 64-row
+    // waves (64x128 in 4-wave blocks, 64x64 in 8-wave blocks), three planes 32-row waves
+    if (prec == 0) tile = 24;
+    else tile = kp.Co > 64 && kp.K > 128 ? 21 : 24;
+  }
+  if (prec == 0) {
+    switch (tile) {
+      case 21: return launch<8, 4, 8, 2, 3>(kp, st);   // 512 x 128, wave 64 x 128
+      case 22: return launch<8, 4, 4, 2, 3>(kp, st);   // 512 x 64,  wave 64 x 64
+      case 23: return launch<8, 2, 8, 2, 3>(kp, st);   // 256 x 128, wave 32 x 128
+      case 24: return launch<4, 4, 8, 2, 3>(kp, st);   // 256 x 128, wave 64 x 128, 4 waves
+      case 25: return launch<8, 4, 8, 2, 2>(kp, st);   // 512 x 128, 2 stages
+      default: return PRPE_EINVAL;
+    }
+  }
+  switch (tile) {
+    case 21: return launch<4, 2, 8, 3, 3>(kp, st);   // 128 x 128, wave 32 x 128, 4 waves
+    case 22: return launch<8, 4, 4, 3, 3>(kp, st);   // 512 x 64,  wave 64 x 64
+    case 23: return launch<8, 2, 8, 3, 3>(kp, st);   // 256 x 128, wave 32 x 128
+    case 24: return launch<8, 2, 4, 3, 3>(kp, st);   // 256 x 64,  wave 32 x 64
+    case 25: return launch<8, 2, 8, 3, 2>(kp, st);   // 256 x 128, 2 stages
+    default: return PRPE_EINVAL;
+  }
+}
+
+}  // namespace prpe_k

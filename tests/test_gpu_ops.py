@@ -243,6 +243,66 @@ def test_conv_fp32_faithful_mode_every_tile(tile):
     torch.testing.assert_close(got, ref, rtol=0, atol=2e-6)
 
 
+WAVE_SHAPES = [
+    (2, 64, 17, 19, 96, 3, 1, 1),       # ragged spatial (M tail inside a wave), ragged Co
+    (2, 128, 11, 9, 64, 3, 2, 1),       # 3x3 / 2
+    (2, 64, 20, 20, 256, 1, 1, 0),      # 1x1, two column tiles
+    (1, 256, 10, 10, 512, 1, 2, 0),     # 1x1 / 2 (downsample)
+    (1, 512, 7, 7, 64, 7, 1, 0),        # 7x7 (IR-50 output linear)
+    (3, 96, 13, 17, 136, 3, 1, 1),      # Co beyond one 128 tile
+]
+
+
+@pytest.mark.parametrize("precision", [0, 2])
+@pytest.mark.parametrize("tile", [21, 22, 23, 24, 25])
+@pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", WAVE_SHAPES)
+def test_conv_wave_kernel_bit_exact_vs_lds_staged(B, Ci, H, W, Co, k, s, p, tile, precision):
+    """conv_wave.hip (A straight into fragment registers, B through an LDS-DMA ring) runs the
+    same K order, plane split and MFMA order per accumulator as the register-staged kernel:
+    the results agree bit for bit, and both match the fp64 reference."""
+    x = rnd(B, Ci, H, W, seed=80)
+    w = rnd(Co, Ci, k, k, seed=81, scale=1.0 / math.sqrt(Ci * k * k))
+    sc = torch.rand(Co, generator=_g(82)) + 0.5
+    bi = rnd(Co, seed=83)
+    kw = dict(act="silu", scale=sc, bias=bi, k_order=1, precision=precision)
+    got = run_conv(x, w, s, p, tile=tile, **kw)
+    base = run_conv(x, w, s, p, tile=5, **kw)
+    assert torch.equal(got, base)
+    ref = ref_conv(x, w, s, p, act="silu", scale=sc, bias=bi)
+    torch.testing.assert_close(got, ref, rtol=0, atol=_tol(x, w) * 2)
+
+
+@pytest.mark.parametrize("mode", [RES_PRE, RES_POST])
+@pytest.mark.parametrize("tile", [21, 23])
+def test_conv_wave_kernel_prologue_residual_prelu(mode, tile):
+    """IR-50 pre-BN prologue (padding taps stay 0) + PReLU + residual through the per-wave
+    epilogue, including a non-linear residual view (subsampled shortcut)."""
+    x = rnd(2, 64, 12, 10, seed=84)
+    w = rnd(96, 64, 3, 3, seed=85, scale=0.05)
+    s_in = torch.rand(64, generator=_g(86)) + 0.5
+    b_in = rnd(64, seed=87)
+    sl = torch.rand(96, generator=_g(88)) * 0.4
+    r = rnd(2, 96, 12, 10, seed=89)
+    kw = dict(act="prelu", slope=sl, in_s=s_in, in_b=b_in, res=r, res_mode=mode, k_order=1, precision=2)
+    got = run_conv(x, w, 1, 1, tile=tile, **kw)
+    assert torch.equal(got, run_conv(x, w, 1, 1, tile=5, **kw))
+    ref = ref_conv(x, w, 1, 1, act="prelu", slope=sl, in_s=s_in, in_b=b_in, res=r, res_mode=mode)
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-5)
+    # stride-2 conv whose residual is a subsampled view of a full-resolution tensor
+    big = rnd(2, 96, 12, 10, seed=90).permute(0, 2, 3, 1).contiguous().to(DEV)
+    rview = big[:, ::2, ::2, :]
+    pk = pack.pack_conv("t", w, 2, 1, DEV, k_order=1)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    outs = []
+    for t in (tile, 5):
+        y = torch.empty(2, 6, 5, 96, device=DEV)
+        ops.conv2d(xd, pk, y, res=rview, res_mode=mode, precision=2, tile=t)
+        outs.append(y.cpu())
+    assert torch.equal(outs[0], outs[1])
+    ref2 = ref_conv(x, w, 2, 1, res=rview.cpu().permute(0, 3, 1, 2), res_mode=mode)
+    torch.testing.assert_close(outs[0].permute(0, 3, 1, 2), ref2, rtol=0, atol=1e-5)
+
+
 def test_conv_fp32_faithful_stem_scalar_path():
     x = rnd(2, 3, 48, 48, seed=48)
     w = rnd(64, 3, 7, 7, seed=49, scale=0.1)

@@ -6,4 +6,4 @@ mkdir -p gpurun_out
 TAG=$1; shift
 export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 -i tools/pmc_conv.txt --kernel-trace -d gpurun_out/pmc_$TAG -o pmc -- python3 tools/conv_bench.py "$@" > gpurun_out/pmc_$TAG.log 2>&1 || { tail -30 gpurun_out/pmc_$TAG.log; exit 1; }
-python tools/pmc_summary.py gpurun_out/pmc_$TAG --kernel conv_igemm --min-us 200
+python tools/pmc_summary.py gpurun_out/pmc_$TAG --kernel "${KFILTER:-conv_}" --min-us 200
