@@ -85,9 +85,23 @@ typedef struct prpe_conv_desc {
   int32_t res_mode;       /* prpe_res_mode */
   int32_t precision;      /* 0 = 2-plane split-bf16, 3 MFMA terms (~2^-17);
                              2 = 3-plane split (exact fp32 operands), 6 terms;
+                             3 = 2-plane split-fp16 with power-of-2 scaling, 3 terms (~2^-21
+                                 per operand: below fp32 accumulation error for K >= 64);
+                                 needs w_h16/w_l16/scale16/x_amax, no in_scale, and a
+                                 channel-chunked input (Ci % 32 == 0, k_order 1 or 1x1);
                              1 = plain bf16 (1 term; diagnostics only) */
-  int32_t tile;           /* 0 = auto; 1..6 = 128x128, 128x64, 128x32, 128x16, 256x128, 256x64 */
+  int32_t tile;           /* 0 = auto; 1..6 = 128x128, 128x64, 128x32, 128x16, 256x128, 256x64
+                             (register-staged); 10..12 LDS-DMA staged; 21..25 wave-row */
   int32_t k_order;        /* weight K order, see above */
+  /* precision 3 operands: fp16 planes [co_pad][k_pad] of w[co][k] * 2^e[co] (w = (h16 + l16)
+   * * 2^-e[co] to ~2^-22), the epilogue scale with 2^-e[co] folded in, and a device scalar
+   * bounding max|x| (the producer's y_amax) that sets the activations' power-of-2 scale */
+  const uint16_t* w_h16;
+  const uint16_t* w_l16;
+  const float* scale16;   /* [Co] */
+  const float* x_amax;
+  float* y_amax;          /* optional (any precision): device scalar raised to max|y| (atomic;
+                             zero it before the producing launch) */
 } prpe_conv_desc;
 
 int prpe_conv2d(const prpe_conv_desc* d, void* stream);

@@ -2,8 +2,12 @@
 // any layout; conv_glds.hip: direct global->LDS staging for channel-chunked inputs).
 #pragma once
 #include "common.h"
+#include <type_traits>
 
 namespace prpe_k {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 
 // Kernel arguments of prpe_conv2d (host-validated, see conv_igemm.hip)
 struct ConvK {
@@ -20,41 +24,95 @@ struct ConvK {
                        // re-load the symbol's address from the GOT every step); 32 zero bytes
   int ylin, rlin;      // y (r) offset of pixel m is m * ysw (rsw): contiguous pixels, so the
                        // epilogue skips the m -> (n, oh, ow) division
+  const uint16_t* wh16; const uint16_t* wl16;   // precision 3: fp16 planes of the scaled weights
+  const float* x_amax;                          // precision 3: upper bound of max|x| (device)
+  float* y_amax;                                // optional: raised to max|y| (device, atomic)
 };
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// max |v| of a float4 (NaN lanes are ignored by fmaxf)
+__device__ __forceinline__ float amax4(f4 v) {
+  return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+}
+// raise *slot to the wave's maximum of m (m >= 0: float order == unsigned bit order); every
+// lane of the wave must call it
+__device__ __forceinline__ void amax_commit(float* slot, float m) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m > 0.f) {
+    // one slot per tensor, so most waves would contend on one address: read it first (an
+    // agent-scope load, past the non-coherent L1) and only raise it when this wave's max is
+    // larger -- the slot only grows, so a stale read can only cost a redundant atomic
+    unsigned* u = reinterpret_cast<unsigned*>(slot);
+    const unsigned b = __float_as_uint(m);
+    if (b > __hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(u, b);
+  }
+}
 
 // F = {0,2,3,1} indexed by (row >> 2) & 3, branch-free
 __device__ __forceinline__ int swzF(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
 
 // native vector types: HIP's float4/uint4 are structs, and arrays of them cannot be promoted
 // to registers (the compiler moved them to a per-thread LDS array with 64-B lane stride)
-typedef float f4 __attribute__((ext_vector_type(4)));
-typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 
 // fp32 x4 -> NP bf16 planes, two lanes at a time: hi = RNE(v) (v_cvt_pk_bf16_f32), its fp32
-// value rebuilt by a shift / mask, remainder by one packed subtract, and so on per plane
-// (the compiler's per-element lowering of the same casts took 13 VALU per float4 at NP 2)
+// value rebuilt by a shift / mask, the (exact) remainder by one scalar v_sub_f32 per element,
+// and so on per plane. The compiler's per-element lowering of the same casts took 13 VALU per
+// float4 at NP 2; its SLP-packed v_pk_add_f32 for the remainder costs extra issue cycles
+// beside MFMAs (MI355X_MICROARCH.md, "price of one filler"), hence the explicit scalar subtract
+// (measured +2..7 % on the MFMA-bound 3x3 convs, bit-identical).
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float sub_f32(float a, float b) {
+  float d;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
 template <int NP>
 __device__ __forceinline__ void split_planes(f4 v, bf16x4 (&pl)[NP]) {
-  f2v r[2] = {f2v{v[0], v[1]}, f2v{v[2], v[3]}};
+  float r[4] = {v[0], v[1], v[2], v[3]};
 #pragma unroll
   for (int q = 0; q < NP; ++q) {
     unsigned u[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const bf16x2v b = __builtin_convertvector(r[h], bf16x2v);
+      const bf16x2v b = __builtin_convertvector(f2v{r[2 * h], r[2 * h + 1]}, bf16x2v);
       u[h] = __builtin_bit_cast(unsigned, b);
       if (q + 1 < NP) {
-        const f2v back = {__builtin_bit_cast(float, u[h] << 16), __builtin_bit_cast(float, u[h] & 0xffff0000u)};
-        r[h] = r[h] - back;
+        r[2 * h] = sub_f32(r[2 * h], __builtin_bit_cast(float, u[h] << 16));
+        r[2 * h + 1] = sub_f32(r[2 * h + 1], __builtin_bit_cast(float, u[h] & 0xffff0000u));
       }
     }
     pl[q] = __builtin_bit_cast(bf16x4, (unsigned long long)u[0] | ((unsigned long long)u[1] << 32));
   }
 }
 
-
+// fp32 x4 -> two fp16 planes (packed 4 x f16 each) of v * sa: hi = RTZ(v sa)
+// (v_cvt_pkrtz_f16_f32), lo = RTZ(v sa - hi) with the remainder exact in fp32; |v sa| < 2^15
+// by the choice of sa, so neither plane overflows and v sa = hi + lo to ~2^-21 relative
+// (lo can be subnormal for tiny v: absolute error <= 2^-25 in scaled units)
+__device__ __forceinline__ void split_planes_f16(f4 v, float sa, unsigned long long (&pl)[2]) {
+  float r[4] = {v[0] * sa, v[1] * sa, v[2] * sa, v[3] * sa};
+  unsigned u[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const auto hi = __builtin_amdgcn_cvt_pkrtz(r[2 * h], r[2 * h + 1]);
+    u[0][h] = __builtin_bit_cast(unsigned, hi);
+    r[2 * h] = sub_f32(r[2 * h], (float)hi[0]);
+    r[2 * h + 1] = sub_f32(r[2 * h + 1], (float)hi[1]);
+    u[1][h] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(r[2 * h], r[2 * h + 1]));
+  }
+#pragma unroll
+  for (int q = 0; q < 2; ++q) pl[q] = (unsigned long long)u[q][0] | ((unsigned long long)u[q][1] << 32);
+}
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;

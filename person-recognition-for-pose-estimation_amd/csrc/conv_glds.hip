@@ -181,6 +181,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_glds_kernel(ConvK p) {
   // ---------------- epilogue (as conv_igemm.hip): C tile staged through LDS, whole-row
   // 16-B column chunks per thread, coalesced residual loads and output stores
   float* ct = reinterpret_cast<float*>(lds);
+  float ymax = 0.f;                            // running max|y| (p.y_amax)
   constexpr int CPR = BN / 4;
   constexpr int RPP = NT / CPR;
   const int cc = tid % CPR;
@@ -237,11 +238,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_glds_kernel(ConvK p) {
           for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
           if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
           *reinterpret_cast<f4*>(p.y + yo[e]) = v;
+          ymax = fmaxf(ymax, amax4(v));
         }
       }
     }
     if (h0 + CH < BM) __syncthreads();
   }
+  if (p.y_amax) amax_commit(p.y_amax, ymax);
 }
 
 template <int BM, int BN, int NW, int NP2_STAGES, int NP3_STAGES>

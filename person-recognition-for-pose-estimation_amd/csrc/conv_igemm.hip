@@ -339,6 +339,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
   }
 
   // ---------------- epilogue
+  float ymax = 0.f;                                   // running max|y| (p.y_amax)
   if (p.vec_out) {
     // Stage the raw accumulator tile through LDS (CH rows per round), then every thread owns
     // 16-B column chunks of whole rows: coalesced float4 residual loads and output stores.
@@ -402,11 +403,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
             for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
             if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
             *reinterpret_cast<f4*>(p.y + yo[e]) = v;
+            ymax = fmaxf(ymax, amax4(v));
           }
         }
       }
       if (h0 + CH < BM) __syncthreads();
     }
+    if (p.y_amax) amax_commit(p.y_amax, ymax);
     return;
   }
   float sc[TN], bi[TN], sl[TN];
@@ -441,9 +444,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
         v = apply_act(v, p.act, sl[j]);
         if (p.res_mode == PRPE_RES_POST_ACT) v += p.r[ro + col * p.rsc];
         p.y[yo + col * p.ysc] = v;
+        ymax = fmaxf(ymax, fabsf(v));
       }
     }
   }
+  if (p.y_amax) amax_commit(p.y_amax, ymax);
 }
 
 // Direct fp32 conv for Co <= 4 (ViT adapter 128->3, YOLO adapter 64->3, head 80->1): a 16-wide
@@ -475,6 +480,7 @@ __global__ __launch_bounds__(256) void conv_smallco_kernel(ConvK p, int lpp_log2
         }
         w[t][e][c] = v;
       }
+  float ymax = 0.f;
   const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int nw = (int)((gridDim.x * blockDim.x) >> 6);
   for (int base = gw * ppw; base < p.M; base += nw * ppw) {
@@ -516,9 +522,11 @@ __global__ __launch_bounds__(256) void conv_smallco_kernel(ConvK p, int lpp_log2
         v = apply_act(v, p.act, p.slope ? p.slope[c] : 0.f);
         if (p.res_mode == PRPE_RES_POST_ACT) v += p.r[ro + c * p.rsc];
         p.y[yo + c * p.ysc] = v;
+        ymax = fmaxf(ymax, fabsf(v));
       }
     }
   }
+  if (p.y_amax) amax_commit(p.y_amax, ymax);
 }
 
 template <int BM, int BN, int WM, int WN, int KM, bool PRO>
@@ -550,9 +558,11 @@ int launch_cfg(const ConvK& kp0, int km, int prec, hipStream_t st) {
 
 extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   if (!d || !view_ok(&d->x) || !view_ok(&d->y) || !d->w_hi) return PRPE_EINVAL;
-  if (d->precision < 0 || d->precision > 2) return PRPE_EINVAL;
-  if (d->precision != 1 && !d->w_lo) return PRPE_EINVAL;
+  if (d->precision < 0 || d->precision > 3) return PRPE_EINVAL;
+  if ((d->precision == 0 || d->precision == 2) && !d->w_lo) return PRPE_EINVAL;
   if (d->precision == 2 && !d->w_lo2) return PRPE_EINVAL;
+  if (d->precision == 3 && (!d->w_h16 || !d->w_l16 || !d->scale16 || !d->x_amax || d->in_scale))
+    return PRPE_EINVAL;
   if (d->kh <= 0 || d->kw <= 0 || d->stride <= 0 || d->pad < 0) return PRPE_EINVAL;
   const prpe_view& x = d->x; const prpe_view& y = d->y;
   if (x.n != y.n) return PRPE_EINVAL;
@@ -599,6 +609,8 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   kp.vec_out = a16(y) && (d->res_mode == PRPE_RES_NONE || a16(d->res)) &&
                (!d->scale || (uintptr_t)d->scale % 16 == 0) && (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
                (!d->slope || (uintptr_t)d->slope % 16 == 0);
+  kp.wh16 = d->w_h16; kp.wl16 = d->w_l16; kp.x_amax = d->x_amax; kp.y_amax = d->y_amax;
+  if (d->precision == 3) kp.scale = d->scale16;
   kp.ylin = y.sh == (int64_t)Wo * y.sw && y.sn == (int64_t)Ho * y.sh;
   kp.rlin = d->res_mode == PRPE_RES_NONE ||
             (d->res.sh == (int64_t)Wo * d->res.sw && d->res.sn == (int64_t)Ho * d->res.sh);
@@ -642,6 +654,11 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const char* e = getenv("PRPE_CONV_WAVE");
     return e && e[0] == '0' ? 0 : 1;
   }();
+  // precision 3 (split fp16) is implemented by the wave-row kernel only
+  if (prec == 3) {
+    if (tile != 0 && tile < 20) return PRPE_EINVAL;
+    return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile ? tile : 20, st) : PRPE_EINVAL;
+  }
   if (tile >= 20) return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile, st) : PRPE_EINVAL;
   if (tile >= 10) return conv_glds_eligible(kp, prec, km) ? conv_glds_launch(kp, prec, tile, st) : PRPE_EINVAL;
   // wave-row kernel everywhere it applies except two-plane Co <= 64, where the LDS-staged

@@ -36,8 +36,15 @@ namespace {
 
 constexpr int BK = 32;
 
-template <int NW, int TM, int TN, int NP, int STAGES, bool PRO>
+// F16 (precision 3): two fp16 planes instead of bf16 ones. The weights arrive pre-scaled per
+// output channel (2^e[co], folded back through the epilogue scale); the activations are
+// scaled by sa = 2^(15 - e) with max|x| < 2^e read from the producer's running maximum
+// (*x_amax), so every scaled value is < 2^15 and the planes stay inside fp16's range: operand
+// error ~2^-22, below fp32's own accumulation error for K >= 64 (Precision).
+template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false>
 __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
+  static_assert(!F16 || (NP == 2 && !PRO), "f16 planes: two planes, no prologue");
+  using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
   constexpr int WTM = TM * 16, BM = NW * WTM, BN = TN * 16;
   constexpr int B_STAGE = NP * BN * 64;               // bf16 [NP][BN][32]
   constexpr int NB_TOT = NP * BN / 16;                // 1-KiB LDS-DMA pieces per stage
@@ -89,7 +96,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     const int q = j / (BN / 16), rb = j % (BN / 16);
     const int nrow = rb * 16 + (lane >> 2);
     const int ch = (lane & 3) ^ swzF(nrow);
-    const uint16_t* plane = q == 0 ? p.whi : (q == 1 ? p.wlo : p.wlo2);
+    const uint16_t* plane = F16 ? (q == 0 ? p.wh16 : p.wl16) : (q == 0 ? p.whi : (q == 1 ? p.wlo : p.wlo2));
     bsrc[i] = plane + (int64_t)(n0 + nrow) * p.k_pad + ch * 8;
     bdst[i] = (q * BN + rb * 16) * 64;
   }
@@ -134,7 +141,17 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     }
   };
 
-  bf16x8 af[NP][TM];
+  // activation scale of the fp16 planes (wave-uniform): max|x| < 2^e -> sa = 2^(15 - e)
+  float sa = 1.f, inv_sa = 1.f;
+  if constexpr (F16) {
+    const float amax = *p.x_amax;
+    int e = 0;
+    (void)frexpf(amax, &e);
+    e = amax > 0.f ? (e < -60 ? -60 : (e > 60 ? 60 : e)) : 15;
+    sa = ldexpf(1.f, 15 - e);
+    inv_sa = ldexpf(1.f, e - 15);
+  }
+  frag_t af[NP][TM];
   auto split_a = [&]() {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -144,12 +161,23 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
         v1 = v1 * as4[1] + ab4[1];
         if (!((amask >> i) & 1u)) { v0 = f4{0.f, 0.f, 0.f, 0.f}; v1 = v0; }   // padding stays 0
       }
-      bf16x4 p0[NP], p1[NP];
-      split_planes<NP>(v0, p0);
-      split_planes<NP>(v1, p1);
+      if constexpr (F16) {
+        unsigned long long p0[2], p1[2];
+        split_planes_f16(v0, sa, p0);
+        split_planes_f16(v1, sa, p1);
 #pragma unroll
-      for (int q = 0; q < NP; ++q)
-        af[q][i] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
+        for (int q = 0; q < 2; ++q) {
+          typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+          af[q][i] = __builtin_bit_cast(f16x8, u64x2{p0[q], p1[q]});
+        }
+      } else {
+        bf16x4 p0[NP], p1[NP];
+        split_planes<NP>(v0, p0);
+        split_planes<NP>(v1, p1);
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+          af[q][i] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
+      }
     }
   };
 
@@ -165,9 +193,9 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     for (int j = 0; j < TN; ++j) {
       const int nrow = j * 16 + fr;
       const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
-      bf16x8 bfr[NP];
+      frag_t bfr[NP];
 #pragma unroll
-      for (int q = 0; q < NP; ++q) bfr[q] = *reinterpret_cast<const bf16x8*>(bp + q * BN * 64);
+      for (int q = 0; q < NP; ++q) bfr[q] = *reinterpret_cast<const frag_t*>(bp + q * BN * 64);
       // partial products smallest first; terms with plane-index sum >= NP are dropped
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -175,7 +203,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
         for (int s = NP - 1; s >= 0; --s)
 #pragma unroll
           for (int qa = s; qa >= 0; --qa)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[qa][i], bfr[s - qa], acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma16(af[qa][i], bfr[s - qa], acc[i][j]);
     }
   };
 
@@ -214,6 +242,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     if (p.bias) bi4 = *reinterpret_cast<const f4*>(p.bias + col);
     if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
   }
+  float ymax = 0.f;                                   // running max|y| (p.y_amax)
   auto offs = [&](int m, int64_t& yo, int64_t& ro) {
     if (p.ylin && p.rlin) {
       yo = (int64_t)m * p.ysw + col;
@@ -252,24 +281,29 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     for (int e = 0; e < EB; ++e) {
       f4 v = *reinterpret_cast<const f4*>(ct + (rr0 + RPP * e) * CS + cc * 4);
       if (!ok[e]) continue;
+      if constexpr (F16) v = v * inv_sa;   // exact (power of two)
       v = v * sc4 + bi4;
       if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
       if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
       *reinterpret_cast<f4*>(p.y + yo[e]) = v;
+      ymax = fmaxf(ymax, amax4(v));
     }
   }
+  if (p.y_amax) amax_commit(p.y_amax, ymax);
 }
 
-template <int NW, int TM, int TN, int NP, int STAGES>
+template <int NW, int TM, int TN, int NP, int STAGES, bool F16 = false>
 int launch(const ConvK& kp0, hipStream_t st) {
   constexpr int BM = NW * TM * 16, BN = TN * 16;
   ConvK kp = kp0;
   const int tiles_m = (kp.M + BM - 1) / BM;
   kp.tiles_n = (kp.Co + BN - 1) / BN;
   kp.nwg = tiles_m * kp.tiles_n;
-  if (kp.in_scale)
+  if constexpr (F16)
+    hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  else if (kp.in_scale)
     hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
   else
     hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
@@ -280,10 +314,12 @@ int launch(const ConvK& kp0, hipStream_t st) {
 
 bool conv_wave_eligible(const ConvK& kp, int prec, int km) {
   // chunk-major K walk (km 2, or any 1x1 on the vector path with whole 32-channel chunks),
-  // vectorised epilogue, precision 0 / 2, K in whole K-steps, B rows readable up to a
-  // multiple of 128
+  // vectorised epilogue, precision 0 / 2 / 3, K in whole K-steps, B rows readable up to a
+  // multiple of 128; precision 3 also needs its fp16 planes and the input's max bound and
+  // has no prologue
   const bool chunked = km == 2 || (km == 1 && kp.KH * kp.KW == 1 && kp.Ci % 32 == 0);
-  return chunked && kp.vec_out && (prec == 0 || prec == 2) && kp.K % BK == 0 && kp.k_pad == kp.K &&
+  const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.in_scale;
+  return chunked && kp.vec_out && (prec == 0 || prec == 2 || p3) && kp.K % BK == 0 && kp.k_pad == kp.K &&
          kp.zero != nullptr;
 }
 
@@ -293,6 +329,7 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
     // measured (tools/conv_bench.py, profiles/r01_conv_bench_wave.txt): two planes want 64-row
     // waves (64x128 in 4-wave blocks, 64x64 in 8-wave blocks), three planes 32-row waves
     if (prec == 0) tile = 24;
+    else if (prec == 3) tile = kp.Co > 64 && kp.K > 128 ? 24 : 25;
     else tile = kp.Co > 64 && kp.K > 128 ? 21 : 24;
   }
   if (prec == 0) {
@@ -302,6 +339,16 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       case 23: return launch<8, 2, 8, 2, 3>(kp, st);   // 256 x 128, wave 32 x 128
       case 24: return launch<4, 4, 8, 2, 3>(kp, st);   // 256 x 128, wave 64 x 128, 4 waves
       case 25: return launch<8, 4, 8, 2, 2>(kp, st);   // 512 x 128, 2 stages
+      default: return PRPE_EINVAL;
+    }
+  }
+  if (prec == 3) {
+    switch (tile) {
+      case 21: return launch<8, 4, 8, 2, 3, true>(kp, st);
+      case 22: return launch<8, 4, 4, 2, 3, true>(kp, st);
+      case 23: return launch<8, 2, 8, 2, 3, true>(kp, st);
+      case 24: return launch<4, 4, 8, 2, 3, true>(kp, st);
+      case 25: return launch<8, 2, 4, 2, 3, true>(kp, st);   // 256 x 64, wave 32 x 64
       default: return PRPE_EINVAL;
     }
   }

@@ -27,12 +27,16 @@ YOLO_BN_EPS = 1e-3
 BN_EPS = 1e-5
 
 
-# Per-component conv precision (prpe_conv2d ``precision``): 2 = 3-plane split, fp32-faithful
-# operands (6 MFMA terms); 0 = 2-plane split (3 terms, ~2^-17). "auto" spends the extra MFMA
-# passes where errors are amplified most (measured, DESIGN.md "Precision"): the ResNet-50 trunk
-# every head consumes, and the small YOLO net whose DFL box decode multiplies logit errors by
-# the stride; the large adapters and the ViT run the 3-term split.
-AUTO_POLICY = {"trunk": 2, "yolo_adapter": 0, "yolo_net": 2, "adaface": 0, "vit": 0}
+# Per-component conv precision (prpe_conv2d ``precision``): 2 = 3-plane bf16 split, exact fp32
+# operands (6 MFMA terms); 3 = 2-plane fp16 split with power-of-2 scaling (3 terms, ~2^-21 per
+# operand, below fp32's own accumulation error; needs a chunked input with a tracked max|x|,
+# else the conv runs precision 2); 0 = 2-plane bf16 split (3 terms, ~2^-17). "auto" keeps
+# fp32-faithful products where errors are amplified most (measured, DESIGN.md "Precision"):
+# the ResNet-50 trunk every head consumes, and the small YOLO net whose DFL box decode
+# multiplies logit errors by the stride; the large adapters and the ViT run the bf16 3-term
+# split.
+AUTO_POLICY = {"trunk": 3, "yolo_adapter": 0, "yolo_net": 2, "adaface": 0, "vit": 0}
+AMAX_SLOTS = 4096
 
 
 class _Prec:
@@ -64,6 +68,8 @@ class Engine:
         self._aux: dict[str, torch.Tensor] = {}
         self.watch: set[str] = set()      # pack names whose launches get HIP-event timing
         self.events: dict[str, list] = {}
+        self._amax_pool = None             # device max|y| slots of conv outputs (precision 3)
+        self._amax_i = 0
 
     def prec(self, comp):
         return _Prec(self, comp)
@@ -99,20 +105,51 @@ class Engine:
             self._packs[name] = p
         return p
 
+    # ---- max|y| tracking: every conv output gets a device slot its epilogue raises to max|y|;
+    # a precision-3 consumer reads it to pick its activation scale. Slots are zeroed once per
+    # forward (amax_reset, at the start of the trunk).
+    def amax_reset(self):
+        if self._amax_pool is None:
+            self._amax_pool = torch.zeros(AMAX_SLOTS, device=self.device, dtype=torch.float32)
+        else:
+            self._amax_pool.zero_()
+        self._amax_i = 0
+
+    def amax_slot(self):
+        if self._amax_pool is None or self._amax_i >= AMAX_SLOTS:
+            self.amax_reset()
+        t = self._amax_pool[self._amax_i:self._amax_i + 1]
+        self._amax_i += 1
+        return t
+
+    @staticmethod
+    def _f16_ok(x, p: ConvPack, out):
+        chunked = p.k_order == 1 or (p.kh * p.kw == 1 and p.ci % 32 == 0)
+        return (chunked and p.in_scale is None and x.stride(3) == 1 and x.data_ptr() % 16 == 0 and
+                out.shape[3] % 4 == 0 and getattr(x, "_prpe_amax", None) is not None)
+
     def conv(self, x, p: ConvPack, out=None, res=None, res_mode=0, act=None):
         B, H, W, _ = x.shape
         Ho = (H + 2 * p.pad - p.kh) // p.stride + 1
         Wo = (W + 2 * p.pad - p.kw) // p.stride + 1
         if out is None:
             out = self.empty(B, Ho, Wo, p.co)
+        prec = self.precision
+        if prec == 3 and not self._f16_ok(x, p, out):
+            prec = 2
+        xa = getattr(x, "_prpe_amax", None) if prec == 3 else None
+        ya = self.amax_slot() if self.precision == 3 else None
+        kw = dict(res=res, res_mode=res_mode, act=act, precision=prec, x_amax=xa, y_amax=ya)
         if p.name in self.watch:          # HIP events around one kernel (bench roofline)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            ops.conv2d(x, p, out, res=res, res_mode=res_mode, act=act, precision=self.precision)
+            ops.conv2d(x, p, out, **kw)
             e1.record()
-            self.events.setdefault(p.name, []).append((e0, e1, B * Ho * Wo, p, self.precision))
-            return out
-        return ops.conv2d(x, p, out, res=res, res_mode=res_mode, act=act, precision=self.precision)
+            self.events.setdefault(p.name, []).append((e0, e1, B * Ho * Wo, p, prec))
+        else:
+            ops.conv2d(x, p, out, **kw)
+        out._prpe_amax = ya
+        return out
 
     def upconv(self, name, x, wkey, size, align_corners, bn=None, bias_key=None, act="none", prelu=None, out=None):
         """conv3x3(pad 1)(bilinear_upsample(x, size)) [+BN] [+act] via the tap rewrite."""
@@ -141,6 +178,7 @@ class Engine:
     def trunk(self, x_nchw, flip_w=False):
         """MultiTaskResNetFeatureExtractor (modify_models.py:427-437), torchvision v1.5.
         ``flip_w``: run on the W-mirrored frames (torch.flip(images, dims=[-1]))."""
+        self.amax_reset()
         with self.prec("trunk"):
             return self._trunk(x_nchw, flip_w)
 
@@ -160,6 +198,7 @@ class Engine:
         B, H, W, C = y.shape
         mp = self.empty(B, (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1, C)
         x = ops.maxpool(y, mp, 3, 2, 1)
+        x._prpe_amax = y._prpe_amax        # max-pooling never raises max|x|
         for li, (planes, blocks, stride) in enumerate(arch.RESNET50_STAGES, 1):
             for b in range(blocks):
                 q = f"backbone.layer{li}.{b}"

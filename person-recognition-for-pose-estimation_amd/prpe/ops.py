@@ -36,9 +36,19 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1)
 
 
-def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, tile=0):
-    """y = EPI(conv(PRO(x))) with a ``ConvPack`` (see prpe.pack)."""
+def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, tile=0, x_amax=None,
+           y_amax=None):
+    """y = EPI(conv(PRO(x))) with a ``ConvPack`` (see prpe.pack).
+
+    precision 3 (split fp16) needs ``x_amax``: a 1-element device tensor bounding max|x| (e.g.
+    the ``y_amax`` its producer raised). ``y_amax`` (any precision): 1-element device tensor the
+    kernel raises to max|y| (zero it first)."""
     d = ConvDesc()
+    if precision == 3:
+        h16, l16, s16 = pack.f16_planes()
+        d.w_h16, d.w_l16, d.scale16 = h16.data_ptr(), l16.data_ptr(), s16.data_ptr()
+        d.x_amax = _ptr(x_amax)
+    d.y_amax = _ptr(y_amax)
     d.x = view(x)
     d.y = view(y)
     d.res = view(res)

@@ -45,10 +45,22 @@ class ConvPack:
     in_bias: torch.Tensor | None = None
     act: str = "none"
     k_order: int = 0
+    f16: tuple | None = None      # (w_h16, w_l16, scale16), built on first precision-3 use
 
     @property
     def flops_per_pixel(self) -> int:
         return 2 * self.co * self.ci * self.kh * self.kw
+
+    def f16_planes(self):
+        """Precision-3 operands (see split_f16_scaled), cached on the pack."""
+        if self.f16 is None:
+            w = (self.w_hi.float() + self.w_lo.float() + self.w_lo2.float()).cpu()   # exact fp32 w
+            h, l, e = split_f16_scaled(w)
+            sc = self.scale.cpu() if self.scale is not None else torch.ones(self.co)
+            s16 = torch.ldexp(sc.float(), -e[: self.co].to(torch.int32)).float()
+            dev = self.w_hi.device
+            self.f16 = (h.contiguous().to(dev), l.contiguous().to(dev), s16.contiguous().to(dev))
+        return self.f16
 
 
 def split_bf16(w: torch.Tensor, planes: int = 3):
@@ -60,6 +72,22 @@ def split_bf16(w: torch.Tensor, planes: int = 3):
         out.append(t)
         r = r - t.float()
     return out
+
+
+def split_f16_scaled(w2d: torch.Tensor):
+    """[co, K] fp32 -> (hi, lo, e): each row scaled by 2^e[co] so its max |w| lies in
+    [2^14, 2^15) (exact), then split into two fp16 planes as uint16 bits: hi = RNE(w 2^e),
+    lo = RNE(w 2^e - hi); w 2^e = hi + lo to ~2^-22 relative (the lo plane may be subnormal for
+    entries far below the row maximum: absolute error <= 2^-25 in scaled units). All-zero rows
+    get e = 0."""
+    w = w2d.float()
+    m = w.abs().amax(1)
+    _, ex = torch.frexp(m)                       # m = f * 2^ex, f in [0.5, 1)
+    e = torch.where(m > 0, 15 - ex, torch.zeros_like(ex)).to(torch.int32)
+    ws = torch.ldexp(w, e.view(-1, 1))
+    hi = ws.to(torch.float16)
+    lo = (ws - hi.float()).to(torch.float16)
+    return hi.view(torch.int16), lo.view(torch.int16), e
 
 
 def bn_affine(sd, prefix, eps, conv_bias=None):

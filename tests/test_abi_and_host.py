@@ -39,6 +39,18 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert L.prpe_attention(None, None, 1, 192, 12, 64, 0.125, None) == -22
     bad = _lib.View(0x1000, 1, 4, 4, 8, 128, 32, 8, 1)
     assert L.prpe_norm_sigmoid(C.byref(bad), C.byref(bad), None) == -22    # > 4 channels
+    # precision 3 without its fp16 planes / input max bound, or with a prologue affine
+    v = _lib.View(0x1000, 1, 4, 4, 32, 512, 128, 32, 1)
+    d = _lib.ConvDesc(x=v, y=v, kh=1, kw=1, stride=1, pad=0, w_hi=0x1000, w_lo=0x1000, w_lo2=0x1000,
+                      k_pad=32, co_pad=128, precision=3)
+    assert L.prpe_conv2d(C.byref(d), None) == -22
+    d.w_h16 = d.w_l16 = d.scale16 = 0x1000
+    assert L.prpe_conv2d(C.byref(d), None) == -22                          # no x_amax
+    d.x_amax = 0x1000
+    d.in_scale = d.in_bias = 0x1000
+    assert L.prpe_conv2d(C.byref(d), None) == -22                          # prologue
+    d.precision = 4
+    assert L.prpe_conv2d(C.byref(d), None) == -22
 
 
 def test_state_dict_spec_is_complete():
@@ -61,6 +73,29 @@ def test_pack_layout_and_split():
                     k = (kh * 3 + kw) * 3 + ci
                     assert abs(full[co, k] - w[co, ci, kh, kw]) <= 2 ** -16 * abs(w[co, ci, kh, kw]) + 1e-30
     assert torch.all(full[5:] == 0) and torch.all(full[:, 27:] == 0)
+
+
+def test_f16_scaled_planes_pack():
+    """precision-3 weight planes: per-row power-of-2 scale puts max|w| in [2^14, 2^15); the two
+    fp16 planes rebuild w to ~2^-22 of the row maximum; the scale folds into the epilogue."""
+    g = torch.Generator().manual_seed(3)
+    w = torch.randn(40, 64, 3, 3, generator=g) * torch.logspace(-4, 2, 40).view(-1, 1, 1, 1)
+    w[7] = 0.0                                           # an all-zero output channel
+    sc = torch.rand(40, generator=g) + 0.5
+    p = pack.pack_conv("t", w, 1, 1, "cpu", scale=sc)
+    h, l, s16 = p.f16_planes()
+    hf, lf = h.view(torch.float16).float(), l.view(torch.float16).float()
+    assert torch.isfinite(hf).all() and torch.isfinite(lf).all()
+    rows = hf[:40].abs().amax(1)
+    nz = torch.arange(40) != 7
+    assert torch.all(rows[nz] >= 2 ** 14) and torch.all(rows[nz] < 2 ** 15)
+    full = (p.w_hi.float() + p.w_lo.float() + p.w_lo2.float())[:40]
+    e = torch.log2(s16 / sc).round()                     # s16 = scale * 2^-e exactly
+    assert torch.equal(s16, torch.ldexp(sc, e.to(torch.int32)))
+    rebuilt = (hf[:40] + lf[:40]) * torch.ldexp(torch.ones(40), e.to(torch.int32)).view(-1, 1)
+    rowmax = full.abs().amax(1, keepdim=True).clamp_min(1e-30)
+    assert ((rebuilt - full).abs() / rowmax).max() < 2 ** -21
+    assert torch.all(hf[7] == 0) and torch.all(lf[7] == 0)
 
 
 def test_upconv_tap_pack_order():

@@ -303,6 +303,101 @@ def test_conv_wave_kernel_prologue_residual_prelu(mode, tile):
     torch.testing.assert_close(outs[0].permute(0, 3, 1, 2), ref2, rtol=0, atol=1e-5)
 
 
+def _conv_p3(x, w, s, p, tile=0, amax=None, **kw):
+    """precision 3 (split fp16, scaled): x_amax = max|x| (or the given bound)."""
+    pk = pack.pack_conv("t", w, s, p, DEV, scale=kw.pop("scale", None), bias=kw.pop("bias", None),
+                        act=kw.pop("act", "none"), k_order=1 if w.shape[2] * w.shape[3] > 1 else 0)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    B, _, H, W = x.shape
+    Ho, Wo = (H + 2 * p - w.shape[2]) // s + 1, (W + 2 * p - w.shape[3]) // s + 1
+    y = torch.empty(B, Ho, Wo, w.shape[0], device=DEV)
+    xa = torch.tensor([float(x.abs().max()) if amax is None else amax], device=DEV)
+    ya = torch.zeros(1, device=DEV)
+    r = kw.pop("res", None)
+    rd = r.permute(0, 2, 3, 1).contiguous().to(DEV) if r is not None else None
+    ops.conv2d(xd, pk, y, res=rd, precision=3, tile=tile, x_amax=xa, y_amax=ya, **kw)
+    torch.cuda.synchronize()
+    return y.permute(0, 3, 1, 2).cpu(), float(ya.item())
+
+
+@pytest.mark.parametrize("tile", [0, 21, 22, 23, 24, 25])
+@pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", WAVE_SHAPES)
+def test_conv_f16_split_fp32_level_accuracy(B, Ci, H, W, Co, k, s, p, tile):
+    """precision 3: per-output error vs fp64 within a few fp32 ulps of sum|x||w| (the CPU's own
+    fp32 conv is the yardstick), far below the 2-plane bf16 split; y_amax == max|y| exactly."""
+    x = torch.relu(rnd(B, Ci, H, W, seed=91)) * 7.0
+    w = rnd(Co, Ci, k, k, seed=92, scale=1.0 / math.sqrt(Ci * k * k))
+    sc = torch.rand(Co, generator=_g(93)) + 0.5
+    bi = rnd(Co, seed=94)
+    got, ymax = _conv_p3(x, w, s, p, tile=tile, scale=sc, bias=bi)
+    ref = ref_conv(x, w, s, p, scale=sc, bias=bi).double()
+    den = F.conv2d(x.double().abs(), w.double().abs(), None, s, p) * sc.double().view(1, -1, 1, 1)
+    e16 = ((got.double() - ref).abs() / den).max().item()
+    cpu = F.conv2d(x, w, None, s, p) * sc.view(1, -1, 1, 1) + bi.view(1, -1, 1, 1)
+    e32 = ((cpu.double() - ref).abs() / den).max().item()
+    bf = run_conv(x, w, s, p, scale=sc, bias=bi, precision=0, k_order=1 if k > 1 else 0)
+    ebf = ((bf.double() - ref).abs() / den).max().item()
+    f32 = run_conv(x, w, s, p, scale=sc, bias=bi, precision=2, k_order=1 if k > 1 else 0)
+    e6 = ((f32.double() - ref).abs() / den).max().item()
+    # the fp32-faithful 6-term mode and the CPU's fp32 conv are the yardsticks
+    assert e16 <= max(3 * e6, 10 * e32, 2.0 ** -22), (e16, e6, e32)
+    # far below the bf16 2-plane split, unless fp32 accumulation dominates both (K = 25088)
+    assert e16 < ebf / 4 or e16 <= 1.5 * e6, (e16, ebf, e6)
+    assert ymax == float(got.abs().max())
+
+
+@pytest.mark.parametrize("amp", [1e-5, 1e-2, 1e2, 1e5])
+def test_conv_f16_split_activation_scaling(amp):
+    """The power-of-2 activation scale follows max|x| over 20 decades: no fp16 overflow at
+    1e5, no lost low plane at 1e-5; a loose (larger) bound only costs low bits."""
+    x = torch.relu(rnd(2, 64, 9, 11, seed=95)) * amp
+    w = rnd(96, 64, 3, 3, seed=96, scale=0.05)
+    ref = ref_conv(x, w, 1, 1).double()
+    den = F.conv2d(x.double().abs(), w.double().abs(), None, 1, 1)
+    for bound in (None, float(x.abs().max()) * 3.9):
+        got, _ = _conv_p3(x, w, 1, 1, amax=bound)
+        assert torch.isfinite(got).all()
+        assert ((got.double() - ref).abs() / den).max().item() < 2 ** -20
+
+
+def test_conv_f16_split_residual_and_chained_amax():
+    """Producer -> consumer: the first conv's y_amax is the second's x_amax (the engine's
+    wiring); residual + ReLU epilogue under precision 3."""
+    x = rnd(2, 64, 10, 10, seed=97)
+    w1 = rnd(128, 64, 1, 1, seed=98, scale=0.2)
+    w2 = rnd(64, 128, 3, 3, seed=99, scale=0.03)
+    r = rnd(2, 64, 10, 10, seed=100)
+    p1 = pack.pack_conv("a", w1, 1, 0, DEV, act="relu")
+    p2 = pack.pack_conv("b", w2, 1, 1, DEV, act="relu", k_order=1)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    xa = torch.tensor([float(x.abs().max())], device=DEV)
+    a1, a2 = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    t = torch.empty(2, 10, 10, 128, device=DEV)
+    ops.conv2d(xd, p1, t, precision=3, x_amax=xa, y_amax=a1)
+    y = torch.empty(2, 10, 10, 64, device=DEV)
+    ops.conv2d(t, p2, y, res=r.permute(0, 2, 3, 1).contiguous().to(DEV), res_mode=RES_PRE, precision=3,
+               x_amax=a1, y_amax=a2)
+    torch.cuda.synchronize()
+    assert a1.item() == t.abs().max().item() and a2.item() == y.abs().max().item()
+    ref = ref_conv(ref_conv(x, w1, 1, 0, act="relu"), w2, 1, 1, act="relu", res=r, res_mode=RES_PRE)
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=2e-6)
+
+
+def test_conv_y_amax_every_kernel_family():
+    """y_amax from the register-staged (scalar and vector epilogues), LDS-DMA and wave-row
+    kernels and the small-Co kernel."""
+    x = rnd(2, 64, 9, 13, seed=101)
+    for co, tile, k in ((150, 5, 3), (152, 5, 3), (152, 10, 3), (152, 21, 3), (3, 0, 1)):
+        w = rnd(co, 64, k, k, seed=102, scale=0.05)
+        pk = pack.pack_conv("t", w, 1, k // 2, DEV, k_order=1 if k > 1 else 0)
+        xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+        y = torch.empty(2, 9, 13, co, device=DEV)
+        ya = torch.zeros(1, device=DEV)
+        ops.conv2d(xd, pk, y, precision=2, tile=tile, y_amax=ya)
+        torch.cuda.synchronize()
+        assert ya.item() == y.abs().max().item(), (co, tile)
+
+
 def test_conv_fp32_faithful_stem_scalar_path():
     x = rnd(2, 3, 48, 48, seed=48)
     w = rnd(64, 3, 7, 7, seed=49, scale=0.1)

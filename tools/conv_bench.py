@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--tiles", default="0")
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--korders", default="0,1", help="weight K orders to compare (1 = chunk-major)")
+    ap.add_argument("--amax", action="store_true", help="also track max|y| (y_amax) in the epilogue")
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -60,19 +61,27 @@ def main():
         y = torch.empty(B, Ho, Wo, Co, device=dev)
         r = torch.rand(B, Ho, Wo, Co, device=dev) if "res" in flags else None
         fl = 2.0 * B * Ho * Wo * Co * Ci * k * k
+        xa = x.abs().max().view(1)
+        ya = torch.zeros(1, device=dev) if a.amax else None
         for (ko, pk) in pks.items():
           for prec in [int(v) for v in a.prec.split(",")]:
             for tile in [int(v) for v in a.tiles.split(",")]:
-                ops.conv2d(x, pk, y, res=r, res_mode=1 if r is not None else 0, precision=prec, tile=tile)
+                kw = dict(res=r, res_mode=1 if r is not None else 0, precision=prec, tile=tile, y_amax=ya,
+                          x_amax=xa if prec == 3 else None)
+                try:
+                    ops.conv2d(x, pk, y, **kw)
+                except Exception as ex:              # tile not eligible for this shape
+                    print(f"{name:40s} ko={ko} prec={prec} tile={tile}   n/a ({ex})", flush=True)
+                    continue
                 torch.cuda.synchronize()
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(a.iters):
-                    ops.conv2d(x, pk, y, res=r, res_mode=1 if r is not None else 0, precision=prec, tile=tile)
+                    ops.conv2d(x, pk, y, **kw)
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.iters
-                passes = {0: 3, 1: 1, 2: 6}[prec]
+                passes = {0: 3, 1: 1, 2: 6, 3: 3}[prec]
                 tf = fl / ms / 1e9
                 print(f"{name:40s} ko={ko} prec={prec} tile={tile} {ms:8.3f} ms  alg {tf:7.1f} TF/s  exec {tf * passes:7.1f} TF/s",
                       flush=True)

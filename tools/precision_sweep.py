@@ -19,7 +19,7 @@ x = synth.frames(2).cuda()
 xb = synth.frames(64).cuda()
 ref_nms = R.non_max_suppression(torch.from_numpy(g["det_face_s8"]))
 cr, _ = R.keypoints_from_heatmaps(torch.from_numpy(g["heatmaps"]))
-POL = [("auto", "auto"), ("trunk=0", {"trunk": 0}), ("yolo_net=0", {"yolo_net": 0}),
+POL = [("auto", "auto"), ("trunk=2", {"trunk": 2}), ("trunk=0", {"trunk": 0}), ("yolo_net=0", {"yolo_net": 0}),
        ("all 0", 0), ("all 2", 2), ("vit=1", {"vit": 1}), ("adaface=1", {"adaface": 1}),
        ("yolo_ad=1", {"yolo_adapter": 1}), ("trunk=1", {"trunk": 1})]
 sel = sys.argv[1:]
