@@ -137,7 +137,7 @@ int prpe_maxpool(const prpe_view* x, const prpe_view* y, int32_t k, int32_t stri
 
 /* Strided copy with channel zero-padding: y[...,c] = c < x.c ? x[...,c] : 0 (e.g. NCHW frames
  * -> NHWC4 for the vectorised stem conv; the 4th channel meets a zero weight column). */
-int prpe_copy_pad(const prpe_view* x, const prpe_view* y, void* stream);
+int prpe_copy_pad(const prpe_view* x, const prpe_view* y, float* y_amax /* optional */, void* stream);
 
 /* Nearest x2 upsample (yolopt DarkFPN nn.Upsample(scale_factor=2), nn.py:195). */
 int prpe_upsample_nearest2x(const prpe_view* x, const prpe_view* y, void* stream);

@@ -63,6 +63,31 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return start + bid / nx;
 }
 
+// max |v| of a float4 (NaN lanes are ignored by fmaxf)
+__device__ __forceinline__ float amax4(f32x4 v) {
+  return fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+}
+// raise *slot to the wave's maximum of m (m >= 0: float order == unsigned bit order); every
+// lane of the wave must call it
+__device__ __forceinline__ void amax_commit(float* slot, float m) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0 && m > 0.f) {
+    // one slot per tensor, so most waves would contend on one address: read it first (an
+    // agent-scope load, past the non-coherent L1) and only raise it when this wave's max is
+    // larger -- the slot only grows, so a stale read can only cost a redundant atomic
+    unsigned* u = reinterpret_cast<unsigned*>(slot);
+    const unsigned b = __float_as_uint(m);
+    if (b > __hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(u, b);
+  }
+}
+
+// F = {0,2,3,1} indexed by (row >> 2) & 3, branch-free
+__device__ __forceinline__ int swzF(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
+
+// native vector types: HIP's float4/uint4 are structs, and arrays of them cannot be promoted
+// to registers (the compiler moved them to a per-thread LDS array with 64-B lane stride)
+
 static inline bool view_ok(const prpe_view* v) {
   return v && v->ptr && v->n > 0 && v->h > 0 && v->w > 0 && v->c > 0;
 }

@@ -486,14 +486,22 @@ __global__ __launch_bounds__(256) void dfl_decode_kernel(DflK p) {
 // ------------------------------------------------------------------------- copy_pad
 // y[n,h,w,c] = c < x.c ? x[n,h,w,c] : 0  (layout change + channel zero-padding, e.g. NCHW
 // frames -> NHWC4 so the 7x7 stem takes the vectorised implicit-GEMM path)
-struct CopyK { prpe_view x, y; int per_row, chunks; };
+// (+ optional max|y| into *y_amax: the stem's precision-3 activation scale)
+struct CopyK { prpe_view x, y; int per_row, chunks; float* y_amax; };
 __global__ __launch_bounds__(256) void copy_pad_kernel(CopyK p) {
   int row, w;
   row_pos(p.chunks, row, w);
-  if (w >= p.per_row) return;
-  const int n = row / p.y.h, h = row - n * p.y.h;
-  float* y = p.y.ptr + voff(p.y, n, h, w, 0);
-  for (int c = 0; c < p.y.c; ++c) y[(int64_t)c * p.y.sc] = c < p.x.c ? p.x.ptr[voff(p.x, n, h, w, c)] : 0.f;
+  float m = 0.f;
+  if (w < p.per_row) {
+    const int n = row / p.y.h, h = row - n * p.y.h;
+    float* y = p.y.ptr + voff(p.y, n, h, w, 0);
+    for (int c = 0; c < p.y.c; ++c) {
+      const float v = c < p.x.c ? p.x.ptr[voff(p.x, n, h, w, c)] : 0.f;
+      y[(int64_t)c * p.y.sc] = v;
+      m = fmaxf(m, fabsf(v));
+    }
+  }
+  if (p.y_amax) amax_commit(p.y_amax, m);
 }
 
 inline unsigned nblocks(int64_t total, int bs = 256) { return (unsigned)((total + bs - 1) / bs); }
@@ -574,9 +582,9 @@ extern "C" int prpe_dwconv(const prpe_view* x, const prpe_view* y, const prpe_vi
   return launch_status();
 }
 
-extern "C" int prpe_copy_pad(const prpe_view* x, const prpe_view* y, void* stream) {
+extern "C" int prpe_copy_pad(const prpe_view* x, const prpe_view* y, float* y_amax, void* stream) {
   if (!view_ok(x) || !view_ok(y) || x->n != y->n || x->h != y->h || x->w != y->w || y->c < x->c) return PRPE_EINVAL;
-  CopyK p{*x, *y, y->w, 0};
+  CopyK p{*x, *y, y->w, 0, y_amax};
   dim3 g;
   if (!rowgrid((int64_t)y->n * y->h, y->w, g, p.chunks)) return PRPE_EINVAL;
   hipLaunchKernelGGL(copy_pad_kernel, g, dim3(256), 0, as_stream(stream), p);

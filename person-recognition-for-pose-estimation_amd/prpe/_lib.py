@@ -53,7 +53,7 @@ SIGNATURES = {
     "prpe_dwconv": (C.c_int, [_VP, _VP, _VP, _P, _I, _I, _I, _P, _P, _I, _P]),
     "prpe_maxpool": (C.c_int, [_VP, _VP, _I, _I, _I, _P]),
     "prpe_upsample_nearest2x": (C.c_int, [_VP, _VP, _P]),
-    "prpe_copy_pad": (C.c_int, [_VP, _VP, _P]),
+    "prpe_copy_pad": (C.c_int, [_VP, _VP, _P, _P]),
     "prpe_norm_sigmoid": (C.c_int, [_VP, _VP, _P]),
     "prpe_layernorm": (C.c_int, [_P, _L, _P, _L, _L, _I, _P, _P, _F, _I, _P]),
     "prpe_attention": (C.c_int, [_P, _P, _I, _I, _I, _I, _F, _P]),

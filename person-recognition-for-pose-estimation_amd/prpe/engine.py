@@ -182,19 +182,41 @@ class Engine:
         with self.prec("trunk"):
             return self._trunk(x_nchw, flip_w)
 
-    def _trunk(self, x_nchw, flip_w=False):
-        # NCHW frames -> NHWC4 (zero 4th channel) so the 7x7/2 stem runs the vectorised
-        # implicit-GEMM path; its weight gets a matching zero input channel
+    def stem(self, x_nchw, flip_w=False):
+        """conv1 7x7/2 pad 3 + bn1 + relu (torchvision resnet50) as a channel-chunked conv.
+
+        The NCHW frames are copied once into a zero-bordered NHWC4 buffer [B, H+6, W+8, 4]
+        (3 rows / columns of padding on each side, 5 extra on the right). Read through the
+        overlapping view V[b, h, w, 32] = buf[b, h, w : w+8, 0:4] (pixel stride 4 floats, 32
+        "channels" = 8 consecutive columns x 4 channels), the stem is a 7x1-tap, stride-2,
+        unpadded conv over 32-channel pixels: one contiguous 128-B row segment per tap, the
+        same chunked implicit GEMM as every other conv (and eligible for precision 3). Its
+        weight is W'[co][kh*32 + kw*4 + c] = W[co, c, kh, kw] (zero for kw = 7 and c = 3)."""
         B0, _, H0, W0 = x_nchw.shape
-        x = ops.copy_pad(ops.nhwc(x_nchw), self.empty(B0, H0, W0, 4), flip_w=flip_w)
+        key = ("stem_buf", B0, H0, W0)
+        buf = self._aux.get(key)
+        if buf is None:
+            for k in [k for k in self._aux if isinstance(k, tuple) and k[0] == "stem_buf"]:
+                del self._aux[k]                       # one batch shape at a time
+            buf = torch.zeros(B0, H0 + 6, W0 + 8, 4, device=self.device, dtype=torch.float32)
+            self._aux[key] = buf
+        amax = self.amax_slot()
+        ops.copy_pad(ops.nhwc(x_nchw), buf[:, 3:3 + H0, 3:3 + W0, :], flip_w=flip_w, y_amax=amax)
+        v = buf.as_strided((B0, H0 + 6, W0, 32), (buf.stride(0), buf.stride(1), 4, 1))
+        v._prpe_amax = amax
         stem = self._packs.get("backbone.conv1")
         if stem is None:
-            w = self.sd["backbone.conv1.weight"].float()
-            w4 = torch.cat([w, torch.zeros(w.shape[0], 1, *w.shape[2:])], 1)
+            w = self.sd["backbone.conv1.weight"].float()             # [64, 3, 7, 7]
+            wv = torch.zeros(w.shape[0], 7, 8, 4)
+            wv[:, :, :7, :3] = w.permute(0, 2, 3, 1)
             s, b = bn_affine(self.sd, "backbone.bn1", BN_EPS)
-            stem = pack_conv("backbone.conv1", w4, 2, 3, self.device, scale=s, bias=b, act="relu")
+            stem = pack_matrix("backbone.conv1", wv.reshape(w.shape[0], 7 * 32), 7, 1, 32, 2, 0, self.device,
+                               scale=s, bias=b, act="relu", k_order=1)
             self._packs["backbone.conv1"] = stem
-        y = self.conv(x, stem)
+        return self.conv(v, stem)
+
+    def _trunk(self, x_nchw, flip_w=False):
+        y = self.stem(x_nchw, flip_w)
         B, H, W, C = y.shape
         mp = self.empty(B, (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1, C)
         x = ops.maxpool(y, mp, 3, 2, 1)

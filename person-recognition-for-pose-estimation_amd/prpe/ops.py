@@ -89,14 +89,15 @@ def maxpool(x, y, k, stride, pad):
     return y
 
 
-def copy_pad(x, y, flip_w=False):
+def copy_pad(x, y, flip_w=False, y_amax=None):
     """y = x zero-padded in C; ``flip_w`` reads x mirrored along W (a negative-stride view,
-    so the flip-test pass needs no flipped copy of the frames)."""
+    so the flip-test pass needs no flipped copy of the frames); ``y_amax`` (1-element device
+    tensor, zeroed) is raised to max|y|."""
     xv = view(x)
     if flip_w:
         xv.ptr = x.data_ptr() + (x.shape[2] - 1) * x.stride(2) * x.element_size()
         xv.sw = -x.stride(2)
-    check(lib().prpe_copy_pad(C.byref(xv), C.byref(view(y)), _stream()), "prpe_copy_pad")
+    check(lib().prpe_copy_pad(C.byref(xv), C.byref(view(y)), _ptr(y_amax), _stream()), "prpe_copy_pad")
     return y
 
 

@@ -98,6 +98,28 @@ def test_f16_scaled_planes_pack():
     assert torch.all(hf[7] == 0) and torch.all(lf[7] == 0)
 
 
+def test_stem_as_chunked_conv_over_overlapping_view():
+    """The engine's stem rewrite (Engine.stem): conv1 7x7/2 pad 3 on NCHW frames equals a
+    7x1-tap stride-2 conv over the 32-"channel" overlapping view of a zero-bordered NHWC4 copy
+    with the re-laid-out weight (evaluated here with torch on the CPU)."""
+    g = torch.Generator().manual_seed(5)
+    B, H, W = 2, 22, 17
+    x = torch.rand(B, 3, H, W, generator=g)
+    w = torch.randn(8, 3, 7, 7, generator=g)
+    buf = torch.zeros(B, H + 6, W + 8, 4)
+    buf[:, 3:3 + H, 3:3 + W, :3] = x.permute(0, 2, 3, 1)
+    v = buf.as_strided((B, H + 6, W, 32), (buf.stride(0), buf.stride(1), 4, 1))
+    wv = torch.zeros(8, 7, 8, 4)
+    wv[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    w2d = wv.reshape(8, 7 * 32)                       # k = kh*32 + kw*4 + c (chunk-major, KW=1)
+    Ho, Wo = (H + 6 - 7) // 2 + 1, (W - 1) // 2 + 1
+    cols = torch.stack([v[:, kh: kh + 2 * Ho - 1: 2, 0: 2 * Wo - 1: 2, :] for kh in range(7)], 3)
+    got = torch.einsum("bhwkc,okc->bohw", cols.double(), w2d.view(8, 7, 32).double())
+    ref = torch.nn.functional.conv2d(x.double(), w.double(), None, 2, 3)
+    assert got.shape == ref.shape
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-12)
+
+
 def test_upconv_tap_pack_order():
     w = torch.randn(4, 6, 3, 3)
     p = pack.pack_upconv_taps("t", w, "cpu")
