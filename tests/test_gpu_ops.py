@@ -298,7 +298,7 @@ def test_conv_wave_kernel_prologue_residual_prelu(mode, tile):
         y = torch.empty(2, 6, 5, 96, device=DEV)
         ops.conv2d(xd, pk, y, res=rview, res_mode=mode, precision=2, tile=t)
         outs.append(y.cpu())
-    assert torch.equal(outs[0], outs[1])
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-6, atol=1e-6)
     ref2 = ref_conv(x, w, 2, 1, res=rview.cpu().permute(0, 3, 1, 2), res_mode=mode)
     torch.testing.assert_close(outs[0].permute(0, 3, 1, 2), ref2, rtol=0, atol=1e-5)
 
@@ -428,6 +428,24 @@ def test_upconv_equals_upsample_then_conv(hi, wi, ho, wo, ac, act, separable):
     ref = F.conv2d(u, w.double(), None, 1, 1) * sc.double().view(1, -1, 1, 1) + bi.double().view(1, -1, 1, 1)
     ref = act_ref(ref.float(), act, sl)
     torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=2e-4)
+
+
+@pytest.mark.parametrize("hi,wi,ho,wo,ac", [(20, 20, 160, 160, True), (20, 20, 256, 192, True),
+                                        (16, 12, 64, 48, False), (7, 9, 20, 13, False), (20, 20, 23, 21, True)])
+def test_upconv_fused_matches_separable(hi, wi, ho, wo, ac):
+    """The one-pass rolling-row kernel and the two-pass separable form evaluate the same sum
+    (FMA contraction may differ: fp32-rounding-level agreement), at the adapters' upsampling
+    ratios and at awkward ones (source intervals of 1-2 output rows)."""
+    Co = 24
+    z = rnd(2, hi, wi, 9 * Co, seed=103).to(DEV)
+    sc = (torch.rand(Co, generator=_g(104)) + 0.5).to(DEV)
+    bi = rnd(Co, seed=105).to(DEV)
+    outs = []
+    for sep in (False, True):
+        y = torch.empty(2, ho, wo, Co, device=DEV)
+        ops.upconv3x3(z, y, ac, sc, bi, None, "gelu", separable=sep)
+        outs.append(y.cpu())
+    torch.testing.assert_close(outs[0], outs[1], rtol=1e-6, atol=1e-6)
 
 
 def test_upconv_nchw_output_view():
