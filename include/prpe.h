@@ -102,6 +102,14 @@ typedef struct prpe_conv_desc {
   const float* x_amax;
   float* y_amax;          /* optional (any precision): device scalar raised to max|y| (atomic;
                              zero it before the producing launch) */
+  /* optional second input (x2.ptr != NULL): y = EPI(W[:, :Ci] x + W[:, Ci:] x2), a 1x1 unpadded
+   * conv over both; x2 is [N, Ho, Wo, C2] on the output's pixel grid (any strides, e.g. a
+   * stride-2 subsampling view), channel-contiguous, C2 % 32 == 0 and Ci % 32 == 0; weights
+   * packed [co_pad][k_pad] with k = Ci + C2 columns; precision 0/2/3 (3 also needs x2_amax;
+   * one activation scale for both inputs). Replaces a ResNet bottleneck's conv3 + downsample
+   * projection + residual add (torchvision resnet50 Bottleneck.forward) with one GEMM. */
+  prpe_view x2;
+  const float* x2_amax;
 } prpe_conv_desc;
 
 int prpe_conv2d(const prpe_conv_desc* d, void* stream);

@@ -27,6 +27,9 @@ struct ConvK {
   const uint16_t* wh16; const uint16_t* wl16;   // precision 3: fp16 planes of the scaled weights
   const float* x_amax;                          // precision 3: upper bound of max|x| (device)
   float* y_amax;                                // optional: raised to max|y| (device, atomic)
+  const float* x2; int64_t x2sn, x2sh, x2sw;    // dual input (conv_wave only), see prpe.h
+  int nk1;                                      // K-steps of the first input
+  const float* x2_amax;
 };
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));

@@ -569,7 +569,17 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   const int Ho = (x.h + 2 * d->pad - d->kh) / d->stride + 1;
   const int Wo = (x.w + 2 * d->pad - d->kw) / d->stride + 1;
   if (Ho != y.h || Wo != y.w) return PRPE_EINVAL;
-  const int K = d->kh * d->kw * x.c;
+  // dual input (x2): 1x1, unpadded, both inputs channel-chunked, K = Ci + C2 in that order
+  const bool dual = d->x2.ptr != nullptr;
+  if (dual) {
+    const prpe_view& v = d->x2;
+    if (!view_ok(&v) || d->kh != 1 || d->kw != 1 || d->pad != 0 || v.n != y.n || v.h != Ho || v.w != Wo ||
+        v.sc != 1 || v.c % 32 || x.c % 32 || v.sw % 4 || v.sh % 4 || v.sn % 4 || (uintptr_t)v.ptr % 16 ||
+        d->in_scale || d->precision == 1 || (d->precision == 3 && !d->x2_amax))
+      return PRPE_EINVAL;
+    if (d->tile != 0 && d->tile < 20) return PRPE_EINVAL;
+  }
+  const int K = d->kh * d->kw * x.c + (dual ? d->x2.c : 0);
   if (d->k_pad % BK || d->k_pad < K || d->co_pad % 128 || d->co_pad < y.c) return PRPE_EINVAL;
   if (d->res_mode != PRPE_RES_NONE && !d->res.ptr) return PRPE_EINVAL;
   if (d->in_scale && !d->in_bias) return PRPE_EINVAL;
@@ -597,6 +607,10 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   kp.r = d->res.ptr; kp.rsn = d->res.sn; kp.rsh = d->res.sh; kp.rsw = d->res.sw; kp.rsc = d->res.sc;
   kp.KH = d->kh; kp.KW = d->kw; kp.stride = d->stride; kp.pad = d->pad;
   kp.K = K; kp.k_pad = d->k_pad; kp.nk = (K + BK - 1) / BK;
+  if (dual) {
+    kp.x2 = d->x2.ptr; kp.x2sn = d->x2.sn; kp.x2sh = d->x2.sh; kp.x2sw = d->x2.sw;
+    kp.nk1 = x.c / BK; kp.x2_amax = d->x2_amax;
+  }
   kp.whi = d->w_hi; kp.wlo = d->w_lo; kp.wlo2 = d->w_lo2;
   kp.scale = d->scale; kp.bias = d->bias; kp.slope = d->slope;
   kp.in_scale = d->in_scale; kp.in_bias = d->in_bias;
@@ -659,7 +673,8 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     if (tile != 0 && tile < 20) return PRPE_EINVAL;
     return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile ? tile : 20, st) : PRPE_EINVAL;
   }
-  if (tile >= 20) return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile, st) : PRPE_EINVAL;
+  if (tile >= 20 || dual)
+    return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile ? tile : 20, st) : PRPE_EINVAL;
   if (tile >= 10) return conv_glds_eligible(kp, prec, km) ? conv_glds_launch(kp, prec, tile, st) : PRPE_EINVAL;
   // wave-row kernel everywhere it applies except two-plane Co <= 64, where the LDS-staged
   // 256x64 tile measured faster (profiles/r01_conv_bench_wave.txt)

@@ -41,9 +41,14 @@ constexpr int BK = 32;
 // scaled by sa = 2^(15 - e) with max|x| < 2^e read from the producer's running maximum
 // (*x_amax), so every scaled value is < 2^15 and the planes stay inside fp16's range: operand
 // error ~2^-22, below fp32's own accumulation error for K >= 64 (Precision).
-template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false>
+// DUAL: two 1x1 inputs summed in one GEMM, y = EPI(W[:, :K1] x + W[:, K1:] x2) (a ResNet
+// bottleneck's conv3 and its downsample projection: the projection is never written to HBM
+// and re-read as the residual). K-steps 0 .. nk1-1 read x, the rest read x2 (a view with the
+// output's pixel grid, e.g. a stride-2 subsampling of the block input).
+template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false>
 __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   static_assert(!F16 || (NP == 2 && !PRO), "f16 planes: two planes, no prologue");
+  static_assert(!DUAL || !PRO, "dual input: no prologue");
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
   constexpr int WTM = TM * 16, BM = NW * WTM, BN = TN * 16;
   constexpr int B_STAGE = NP * BN * 64;               // bf16 [NP][BN][32]
@@ -65,12 +70,14 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
 
   // ---- A rows of this lane: wrow0 + 16 i + fr; element offset of tap (0,0) at channel 8 fg
   int64_t rbase[TM];
+  int64_t rbase2[DUAL ? TM : 1];
   unsigned hmask[TM], wmask[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wrow0 + i * 16 + fr;
     unsigned hm = 0, wmk = 0;
     int64_t b = 0;
+    if constexpr (DUAL) rbase2[i] = 0;
     if (m < p.M) {
       const int n = m / p.HoWo;
       const int rem = m - n * p.HoWo;
@@ -78,6 +85,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       const int ow = rem - oh * p.Wo;
       const int ih = oh * p.stride - p.pad, iw = ow * p.stride - p.pad;
       b = (int64_t)n * p.xsn + (int64_t)ih * p.xsh + (int64_t)iw * p.xsw + fg * 8;
+      if constexpr (DUAL) rbase2[i] = (int64_t)n * p.x2sn + (int64_t)oh * p.x2sh + (int64_t)ow * p.x2sw + fg * 8;
       for (int t = 0; t < p.KH; ++t) hm |= (unsigned)((unsigned)(ih + t) < (unsigned)p.Hi) << t;
       for (int t = 0; t < p.KW; ++t) wmk |= (unsigned)((unsigned)(iw + t) < (unsigned)p.Wi) << t;
     }
@@ -121,10 +129,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       ab4[1] = *reinterpret_cast<const f4*>(p.in_bias + u_ci + fg * 8 + 4);
     }
     amask = 0;
+    const bool second = DUAL && u_step >= p.nk1;     // wave-uniform
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const bool ok = (hmask[i] >> u_kh) & (wmask[i] >> u_kw) & 1u;
-      const float* src = ok ? p.x + (rbase[i] + u_off) : p.zero;
+      const float* src;
+      if constexpr (DUAL)
+        src = !ok ? p.zero : (second ? p.x2 + (rbase2[i] + (u_off - (int64_t)p.nk1 * BK)) : p.x + (rbase[i] + u_off));
+      else
+        src = ok ? p.x + (rbase[i] + u_off) : p.zero;
       raw[i][0] = *reinterpret_cast<const f4*>(src);
       raw[i][1] = *reinterpret_cast<const f4*>(src + 4);
       if constexpr (PRO) amask |= (unsigned)ok << i;
@@ -144,7 +157,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   // activation scale of the fp16 planes (wave-uniform): max|x| < 2^e -> sa = 2^(15 - e)
   float sa = 1.f, inv_sa = 1.f;
   if constexpr (F16) {
-    const float amax = *p.x_amax;
+    const float amax = DUAL ? fmaxf(*p.x_amax, *p.x2_amax) : *p.x_amax;   // one scale for both inputs
     int e = 0;
     (void)frexpf(amax, &e);
     e = amax > 0.f ? (e < -60 ? -60 : (e > 60 ? 60 : e)) : 15;
@@ -301,6 +314,13 @@ int launch(const ConvK& kp0, hipStream_t st) {
   const int tiles_m = (kp.M + BM - 1) / BM;
   kp.tiles_n = (kp.Co + BN - 1) / BN;
   kp.nwg = tiles_m * kp.tiles_n;
+  if (kp.x2) {
+    if constexpr (F16)
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+    else
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, false, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+    return launch_status();
+  }
   if constexpr (F16)
     hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
   else if (kp.in_scale)
@@ -318,7 +338,7 @@ bool conv_wave_eligible(const ConvK& kp, int prec, int km) {
   // multiple of 128; precision 3 also needs its fp16 planes and the input's max bound and
   // has no prologue
   const bool chunked = km == 2 || (km == 1 && kp.KH * kp.KW == 1 && kp.Ci % 32 == 0);
-  const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.in_scale;
+  const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.in_scale && (!kp.x2 || kp.x2_amax);
   return chunked && kp.vec_out && (prec == 0 || prec == 2 || p3) && kp.K % BK == 0 && kp.k_pad == kp.K &&
          kp.zero != nullptr;
 }

@@ -128,18 +128,37 @@ class Engine:
         return (chunked and p.in_scale is None and x.stride(3) == 1 and x.data_ptr() % 16 == 0 and
                 out.shape[3] % 4 == 0 and getattr(x, "_prpe_amax", None) is not None)
 
-    def conv(self, x, p: ConvPack, out=None, res=None, res_mode=0, act=None):
+    def pk_dual(self, q) -> ConvPack:
+        """Bottleneck ``q`` (block 0 of a stage): relu(bn3(conv3(o)) + bn_ds(downsample(x))) as
+        one 1x1 GEMM over [o | x_sub] with each BN scale folded into its weight rows
+        (W' = [s3 W3 | sd Wd], bias b3 + bd; torchvision Bottleneck.forward)."""
+        name = q + ".conv3+downsample"
+        p = self._packs.get(name)
+        if p is None:
+            sd = self.sd
+            w3 = sd[q + ".conv3.weight"].float().flatten(1)
+            wd = sd[q + ".downsample.0.weight"].float().flatten(1)
+            s3, b3 = bn_affine(sd, q + ".bn3", BN_EPS)
+            sdn, bd = bn_affine(sd, q + ".downsample.1", BN_EPS)
+            w = torch.cat([w3 * s3[:, None], wd * sdn[:, None]], 1)
+            p = pack_matrix(name, w, 1, 1, w.shape[1], 1, 0, self.device, bias=b3 + bd, act="relu")
+            self._packs[name] = p
+        return p
+
+    def conv(self, x, p: ConvPack, out=None, res=None, res_mode=0, act=None, x2=None, x2_amax=None):
+        """``x2``: second 1x1 input on the output grid (dual-input GEMM, see prpe.h)."""
         B, H, W, _ = x.shape
         Ho = (H + 2 * p.pad - p.kh) // p.stride + 1
         Wo = (W + 2 * p.pad - p.kw) // p.stride + 1
         if out is None:
             out = self.empty(B, Ho, Wo, p.co)
         prec = self.precision
-        if prec == 3 and not self._f16_ok(x, p, out):
+        if prec == 3 and (not self._f16_ok(x, p, out) or (x2 is not None and x2_amax is None)):
             prec = 2
         xa = getattr(x, "_prpe_amax", None) if prec == 3 else None
         ya = self.amax_slot() if self.precision == 3 else None
-        kw = dict(res=res, res_mode=res_mode, act=act, precision=prec, x_amax=xa, y_amax=ya)
+        kw = dict(res=res, res_mode=res_mode, act=act, precision=prec, x_amax=xa, y_amax=ya, x2=x2,
+                  x2_amax=x2_amax if prec == 3 else None)
         if p.name in self.watch:          # HIP events around one kernel (bench roofline)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -228,12 +247,13 @@ class Engine:
                 o = self.conv(x, self.pk(q + ".conv1", q + ".conv1.weight", bn=q + ".bn1", act="relu"))
                 o = self.conv(o, self.pk(q + ".conv2", q + ".conv2.weight", s, 1, bn=q + ".bn2", act="relu"))
                 if b == 0:
-                    idt = self.conv(x, self.pk(q + ".downsample", q + ".downsample.0.weight", s, 0,
-                                               bn=q + ".downsample.1"))
+                    # conv3 + bn3 and the downsample projection + its BN summed in one dual-input
+                    # GEMM: the projection never goes to HBM as a residual tensor
+                    xs = x if s == 1 else x[:, ::s, ::s, :]
+                    x = self.conv(o, self.pk_dual(q), x2=xs, x2_amax=getattr(x, "_prpe_amax", None))
                 else:
-                    idt = x
-                x = self.conv(o, self.pk(q + ".conv3", q + ".conv3.weight", bn=q + ".bn3", act="relu"),
-                              res=idt, res_mode=RES_PRE)
+                    x = self.conv(o, self.pk(q + ".conv3", q + ".conv3.weight", bn=q + ".bn3", act="relu"),
+                                  res=x, res_mode=RES_PRE)
         return x
 
     # ------------------------------------------------------------------ YOLO v11n branch

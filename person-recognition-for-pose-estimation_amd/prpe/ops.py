@@ -37,7 +37,7 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
 
 
 def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, tile=0, x_amax=None,
-           y_amax=None):
+           y_amax=None, x2=None, x2_amax=None):
     """y = EPI(conv(PRO(x))) with a ``ConvPack`` (see prpe.pack).
 
     precision 3 (split fp16) needs ``x_amax``: a 1-element device tensor bounding max|x| (e.g.
@@ -49,6 +49,9 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
         d.w_h16, d.w_l16, d.scale16 = h16.data_ptr(), l16.data_ptr(), s16.data_ptr()
         d.x_amax = _ptr(x_amax)
     d.y_amax = _ptr(y_amax)
+    if x2 is not None:                 # second 1x1 input, see prpe.h (dual input)
+        d.x2 = view(x2)
+        d.x2_amax = _ptr(x2_amax)
     d.x = view(x)
     d.y = view(y)
     d.res = view(res)

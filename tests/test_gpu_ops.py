@@ -383,6 +383,46 @@ def test_conv_f16_split_residual_and_chained_amax():
     torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=2e-6)
 
 
+@pytest.mark.parametrize("precision", [0, 2, 3])
+@pytest.mark.parametrize("stride,cin,c2,co", [(1, 64, 64, 256), (2, 128, 256, 512), (2, 64, 32, 96)])
+def test_conv_dual_input_bottleneck_projection(precision, stride, cin, c2, co):
+    """Dual-input 1x1 GEMM (ResNet block 0): relu(s3*(W3 o) + b3 + sd*(Wd x[::s, ::s]) + bd) with
+    the BN scales folded into [W3 | Wd]; x2 is a subsampling view of the block input."""
+    B, H, W = 2, 10, 12
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    o = torch.relu(rnd(B, cin, Ho, Wo, seed=106))
+    xb = torch.relu(rnd(B, c2, H, W, seed=107))
+    w3 = rnd(co, cin, 1, 1, seed=108, scale=0.1)
+    wd = rnd(co, c2, 1, 1, seed=109, scale=0.1)
+    s3, b3 = torch.rand(co, generator=_g(110)) + 0.5, rnd(co, seed=111)
+    sd_, bd = torch.rand(co, generator=_g(112)) + 0.5, rnd(co, seed=113)
+    w = torch.cat([w3.flatten(1) * s3[:, None], wd.flatten(1) * sd_[:, None]], 1)
+    pk = pack.pack_matrix("d", w, 1, 1, cin + c2, 1, 0, DEV, bias=b3 + bd, act="relu")
+    od = o.permute(0, 2, 3, 1).contiguous().to(DEV)
+    xd = xb.permute(0, 2, 3, 1).contiguous().to(DEV)
+    x2 = xd[:, ::stride, ::stride, :]
+    y = torch.empty(B, Ho, Wo, co, device=DEV)
+    amax = lambda t: torch.tensor([float(t.abs().max())], device=DEV)
+    ops.conv2d(od, pk, y, precision=precision, x2=x2, x_amax=amax(o), x2_amax=amax(xb))
+    torch.cuda.synchronize()
+    ref = torch.relu(ref_conv(o, w3, 1, 0, scale=s3, bias=b3).double() +
+                     ref_conv(xb, wd, stride, 0, scale=sd_, bias=bd).double()).float()
+    tol = 2e-4 if precision == 0 else 2e-6
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=tol)
+
+
+def test_conv_dual_input_rejects_bad_geometry():
+    o = rnd(1, 64, 5, 5, seed=114).permute(0, 2, 3, 1).contiguous().to(DEV)
+    w = rnd(64, 96, 1, 1, seed=115)
+    pk = pack.pack_conv("t", w, 1, 0, DEV)
+    y = torch.empty(1, 5, 5, 64, device=DEV)
+    with pytest.raises(PrpeError):                       # x2 not on the output grid
+        ops.conv2d(o, pk, y, x2=torch.zeros(1, 6, 5, 32, device=DEV))
+    with pytest.raises(PrpeError):                       # C2 % 32 != 0
+        ops.conv2d(o, pack.pack_conv("t", rnd(64, 80, 1, 1, seed=116), 1, 0, DEV), y,
+                   x2=torch.zeros(1, 5, 5, 16, device=DEV))
+
+
 def test_conv_y_amax_every_kernel_family():
     """y_amax from the register-staged (scalar and vector epilogues), LDS-DMA and wave-row
     kernels and the small-Co kernel."""
