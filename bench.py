@@ -154,6 +154,15 @@ def main():
                              else "inside the timed region"),
                 "in_timed_region_ms": round(sum(timed_ms) / len(timed_ms), 4) if timed_ms else None,
                 "algorithmic_gflop_per_launch": round(fl / 1e9, 2), "traffic": None}
+        # HBM bytes per launch from the PMC passes committed under profiles/ (same kernel, layer
+        # and batch; rocprofv3 cannot run inside this process): tools/run_traffic.sh
+        tp = os.path.join(ROOT, "profiles", "r01_pmc_traffic_dominant.json")
+        if os.path.exists(tp) and B == 256 and args.dominant == "vit_pose.adapter.7":
+            t = json.load(open(tp))
+            roof["traffic"] = round(t["hbm_bytes_per_launch"] / 1e9, 3)
+            roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+            roof["algorithmic_gb_per_launch"] = round(t["algorithmic_bytes_per_launch"] / 1e9, 3)
+            roof["traffic_source"] = "profiles/r01_pmc_traffic_dominant.json"
 
     # ---- CPU baseline (oracle restatement of the reference) + OKS delta, rank 0, N=1 only
     cpu = None

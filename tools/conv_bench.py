@@ -30,6 +30,8 @@ SHAPES = {
     "vit fc1 768->3072 (192 tok)": (16, 12, 768, 3072, 1, 1, 0),
     "vit fc2 3072->768 (192 tok)": (16, 12, 3072, 768, 1, 1, 0),
     "ada_adapter.7 3x3 256->128 @112": (112, 112, 256, 128, 3, 1, 1),
+    "vit_adapter.10 3x3 128->3 @256x192": (256, 192, 128, 3, 3, 1, 1),
+    "yolo_adapter.16 3x3 64->3 @160": (160, 160, 64, 3, 3, 1, 1),
 }
 
 
