@@ -30,6 +30,7 @@
 // Epilogue: each wave stages its accumulator rows through a private 16-row LDS slice and
 // writes whole-row 16-B vectors (scale/bias, act, residual), no block barrier.
 #include "conv.h"
+#include <stdlib.h>
 
 namespace prpe_k {
 namespace {
@@ -346,10 +347,17 @@ bool conv_wave_eligible(const ConvK& kp, int prec, int km) {
 // tile 20 = auto; 21.. force a configuration (tools/conv_bench.py sweeps them)
 int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
   if (tile == 20) {
-    // measured (tools/conv_bench.py, profiles/r01_conv_bench_wave.txt): two planes want 64-row
-    // waves (64x128 in 4-wave blocks, 64x64 in 8-wave blocks), three planes 32-row waves
-    if (prec == 0) tile = 24;
-    else if (prec == 3) tile = kp.Co > 64 && kp.K > 128 ? 24 : 25;
+    // measured (tools/conv_bench.py, profiles/r01_conv_bench_wave.txt, r01_conv_bench_tiles_v3.txt):
+    // two planes run 32x128 waves in 4-wave 128x128 blocks (3 waves/SIMD: more blocks in
+    // flight, finer tail on the ViT / IR-50 GEMM shapes), short-K or narrow convs the 256x64
+    // tile; three bf16 planes 32-row waves
+    // PRPE_WAVE_WIDE=<tile> in the environment overrides the wide-shape choice (A/B runs)
+    static const int wide = [] {
+      const char* e = getenv("PRPE_WAVE_WIDE");
+      return e ? atoi(e) : 26;
+    }();
+    if (prec == 0) tile = wide;
+    else if (prec == 3) tile = kp.Co > 64 && kp.K > 128 ? wide : 25;
     else tile = kp.Co > 64 && kp.K > 128 ? 21 : 24;
   }
   if (prec == 0) {
@@ -359,6 +367,8 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       case 23: return launch<8, 2, 8, 2, 3>(kp, st);   // 256 x 128, wave 32 x 128
       case 24: return launch<4, 4, 8, 2, 3>(kp, st);   // 256 x 128, wave 64 x 128, 4 waves
       case 25: return launch<8, 4, 8, 2, 2>(kp, st);   // 512 x 128, 2 stages
+      case 26: return launch<4, 2, 8, 2, 3>(kp, st);   // 128 x 128, wave 32 x 128, 4 waves
+      case 27: return launch<2, 4, 8, 2, 3>(kp, st);   // 128 x 128, wave 64 x 128, 2 waves
       default: return PRPE_EINVAL;
     }
   }
@@ -369,6 +379,7 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       case 23: return launch<8, 2, 8, 2, 3, true>(kp, st);
       case 24: return launch<4, 4, 8, 2, 3, true>(kp, st);
       case 25: return launch<8, 2, 4, 2, 3, true>(kp, st);   // 256 x 64, wave 32 x 64
+      case 26: return launch<4, 2, 8, 2, 3, true>(kp, st);   // 128 x 128, wave 32 x 128, 4 waves
       default: return PRPE_EINVAL;
     }
   }
@@ -378,6 +389,7 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
     case 23: return launch<8, 2, 8, 3, 3>(kp, st);   // 256 x 128, wave 32 x 128
     case 24: return launch<8, 2, 4, 3, 3>(kp, st);   // 256 x 64,  wave 32 x 64
     case 25: return launch<8, 2, 8, 3, 2>(kp, st);   // 256 x 128, 2 stages
+    case 26: return launch<4, 2, 8, 3, 3>(kp, st);   // = 21 (128 x 128, 4 waves)
     default: return PRPE_EINVAL;
   }
 }

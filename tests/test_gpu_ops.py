@@ -254,7 +254,7 @@ WAVE_SHAPES = [
 
 
 @pytest.mark.parametrize("precision", [0, 2])
-@pytest.mark.parametrize("tile", [21, 22, 23, 24, 25])
+@pytest.mark.parametrize("tile", [21, 22, 23, 24, 25, 26])
 @pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", WAVE_SHAPES)
 def test_conv_wave_kernel_bit_exact_vs_lds_staged(B, Ci, H, W, Co, k, s, p, tile, precision):
     """conv_wave.hip (A straight into fragment registers, B through an LDS-DMA ring) runs the
@@ -320,7 +320,7 @@ def _conv_p3(x, w, s, p, tile=0, amax=None, **kw):
     return y.permute(0, 3, 1, 2).cpu(), float(ya.item())
 
 
-@pytest.mark.parametrize("tile", [0, 21, 22, 23, 24, 25])
+@pytest.mark.parametrize("tile", [0, 21, 22, 23, 24, 25, 26])
 @pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", WAVE_SHAPES)
 def test_conv_f16_split_fp32_level_accuracy(B, Ci, H, W, Co, k, s, p, tile):
     """precision 3: per-output error vs fp64 within a few fp32 ulps of sum|x||w| (the CPU's own

@@ -31,6 +31,9 @@ SHAPES = {
     "vit fc2 3072->768 (192 tok)": (16, 12, 3072, 768, 1, 1, 0),
     "ada_adapter.7 3x3 256->128 @112": (112, 112, 256, 128, 3, 1, 1),
     "vit_adapter.10 3x3 128->3 @256x192": (256, 192, 128, 3, 3, 1, 1),
+    "ir50 body 3x3 256->256 @14": (14, 14, 256, 256, 3, 1, 1),
+    "vit qkv 768->2304 (192 tok)": (16, 12, 768, 2304, 1, 1, 0),
+    "vit proj 768->768 (192 tok)": (16, 12, 768, 768, 1, 1, 0),
     "yolo_adapter.16 3x3 64->3 @160": (160, 160, 64, 3, 3, 1, 1),
 }
 
