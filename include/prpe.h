@@ -110,6 +110,14 @@ typedef struct prpe_conv_desc {
    * projection + residual add (torchvision resnet50 Bottleneck.forward) with one GEMM. */
   prpe_view x2;
   const float* x2_amax;
+  /* planes format: a tensor of fp32 shape [N,H,W,C] whose bytes hold, per pixel and per
+   * group of 8 channels, the 8 bf16 hi planes then the 8 bf16 lo planes of the two-plane split
+   * (hi = RNE(v), lo = RNE(v - hi)): what precision 0 would compute from the fp32 values, so a
+   * producer that writes it saves the consumer's split, bit for bit. x_planes: x is in it
+   * (precision 0, channel-chunked 1x1/3x3, wave-row kernel); y_planes: write y in it
+   * (channel-contiguous, C % 8 == 0, 32-B aligned). */
+  int32_t x_planes;
+  int32_t y_planes;
 } prpe_conv_desc;
 
 int prpe_conv2d(const prpe_conv_desc* d, void* stream);
@@ -125,12 +133,14 @@ int prpe_conv2d(const prpe_conv_desc* d, void* stream);
  * workspace = NULL (the product path) selects the fused one-pass kernel: x-interpolated
  * source rows are kept in rolling registers, HBM traffic = y write + z read. With a workspace
  * of >= prpe_upconv3x3_workspace_bytes(z, y) bytes the sum is instead evaluated in two passes
- * through it (x-interpolation, then y; kept for ablation). Both give identical results.
+ * through it (x-interpolation, then y; kept for ablation). Both agree to fp32 rounding.
+ * y_planes: write y in the planes format of prpe_conv_desc (fused path, C % 8 == 0,
+ * channel-contiguous, 32-B aligned) for a precision-0 consumer conv.
  */
 int64_t prpe_upconv3x3_workspace_bytes(const prpe_view* z, const prpe_view* y);
 int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,
                    const float* scale, const float* bias, const float* slope, int32_t act,
-                   void* workspace, int64_t workspace_bytes, void* stream);
+                   int32_t y_planes, void* workspace, int64_t workspace_bytes, void* stream);
 
 /* Depthwise kxk conv (groups = C) + folded BN + act (+ post-act residual add when res.ptr).
  * Replaces yolopt Conv(g=ch) (nn.py:108, :248-250). */

@@ -30,6 +30,7 @@ struct ConvK {
   const float* x2; int64_t x2sn, x2sh, x2sw;    // dual input (conv_wave only), see prpe.h
   int nk1;                                      // K-steps of the first input
   const float* x2_amax;
+  int x_planes, y_planes;                       // planes format input / output (conv_wave)
 };
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));

@@ -624,6 +624,12 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
                (!d->scale || (uintptr_t)d->scale % 16 == 0) && (!d->bias || (uintptr_t)d->bias % 16 == 0) &&
                (!d->slope || (uintptr_t)d->slope % 16 == 0);
   kp.wh16 = d->w_h16; kp.wl16 = d->w_l16; kp.x_amax = d->x_amax; kp.y_amax = d->y_amax;
+  // planes format (see prpe.h): the wave-row kernel reads / writes it, two bf16 planes only
+  kp.x_planes = d->x_planes; kp.y_planes = d->y_planes;
+  if (d->x_planes && (d->precision != 0 || x.sc != 1 || x.c % 32 || d->in_scale || dual)) return PRPE_EINVAL;
+  if (d->y_planes && (y.sc != 1 || y.c % 8 || y.sw % 8 || y.sh % 8 || y.sn % 8 || (uintptr_t)y.ptr % 32 ||
+                      d->precision == 1))
+    return PRPE_EINVAL;
   if (d->precision == 3) kp.scale = d->scale16;
   kp.ylin = y.sh == (int64_t)Wo * y.sw && y.sn == (int64_t)Ho * y.sh;
   kp.rlin = d->res_mode == PRPE_RES_NONE ||
@@ -673,7 +679,7 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     if (tile != 0 && tile < 20) return PRPE_EINVAL;
     return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile ? tile : 20, st) : PRPE_EINVAL;
   }
-  if (tile >= 20 || dual)
+  if (tile >= 20 || dual || d->x_planes || d->y_planes)
     return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile ? tile : 20, st) : PRPE_EINVAL;
   if (tile >= 10) return conv_glds_eligible(kp, prec, km) ? conv_glds_launch(kp, prec, tile, st) : PRPE_EINVAL;
   // wave-row kernel everywhere it applies except two-plane Co <= 64, where the LDS-staged

@@ -46,8 +46,12 @@ constexpr int BK = 32;
 // bottleneck's conv3 and its downsample projection: the projection is never written to HBM
 // and re-read as the residual). K-steps 0 .. nk1-1 read x, the rest read x2 (a view with the
 // output's pixel grid, e.g. a stride-2 subsampling of the block input).
-template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false>
+// APL: the input tensor is stored as interleaved bf16 planes (see prpe.h, "planes format"):
+// the 32 bytes a lane loads for 8 channels already are the hi and lo fragments, no split.
+template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false,
+          bool APL = false>
 __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
+  static_assert(!APL || (NP == 2 && !F16 && !PRO && !DUAL), "planes input: two bf16 planes only");
   static_assert(!F16 || (NP == 2 && !PRO), "f16 planes: two planes, no prologue");
   static_assert(!DUAL || !PRO, "dual input: no prologue");
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
@@ -175,7 +179,10 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
         v1 = v1 * as4[1] + ab4[1];
         if (!((amask >> i) & 1u)) { v0 = f4{0.f, 0.f, 0.f, 0.f}; v1 = v0; }   // padding stays 0
       }
-      if constexpr (F16) {
+      if constexpr (APL) {
+        af[0][i] = __builtin_bit_cast(bf16x8, v0);
+        af[1][i] = __builtin_bit_cast(bf16x8, v1);
+      } else if constexpr (F16) {
         unsigned long long p0[2], p1[2];
         split_planes_f16(v0, sa, p0);
         split_planes_f16(v1, sa, p1);
@@ -301,7 +308,16 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
       if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
-      *reinterpret_cast<f4*>(p.y + yo[e]) = v;
+      if (p.y_planes) {
+        // planes format: channel group g = c / 8 of a pixel holds hi[8] then lo[8] (bf16)
+        bf16x4 pl[2];
+        split_planes<2>(v, pl);
+        uint16_t* y16 = reinterpret_cast<uint16_t*>(p.y) + 2 * (yo[e] - col) + (col >> 3) * 16 + (col & 7);
+        *reinterpret_cast<bf16x4*>(y16) = pl[0];
+        *reinterpret_cast<bf16x4*>(y16 + 8) = pl[1];
+      } else {
+        *reinterpret_cast<f4*>(p.y + yo[e]) = v;
+      }
       ymax = fmaxf(ymax, amax4(v));
     }
   }
@@ -322,6 +338,12 @@ int launch(const ConvK& kp0, hipStream_t st) {
       hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, false, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
     return launch_status();
   }
+  if (kp.x_planes) {
+    if constexpr (F16 || NP != 2) return PRPE_EINVAL;
+    else hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, false, false, true>), dim3(kp.nwg),
+                            dim3(NW * 64), 0, st, kp);
+    return launch_status();
+  }
   if constexpr (F16)
     hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
   else if (kp.in_scale)
@@ -340,8 +362,9 @@ bool conv_wave_eligible(const ConvK& kp, int prec, int km) {
   // has no prologue
   const bool chunked = km == 2 || (km == 1 && kp.KH * kp.KW == 1 && kp.Ci % 32 == 0);
   const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.in_scale && (!kp.x2 || kp.x2_amax);
+  const bool planes_ok = !kp.x_planes || (prec == 0 && !kp.in_scale && !kp.x2);
   return chunked && kp.vec_out && (prec == 0 || prec == 2 || p3) && kp.K % BK == 0 && kp.k_pad == kp.K &&
-         kp.zero != nullptr;
+         kp.zero != nullptr && planes_ok;
 }
 
 // tile 20 = auto; 21.. force a configuration (tools/conv_bench.py sweeps them)

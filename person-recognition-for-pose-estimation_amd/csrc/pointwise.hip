@@ -50,6 +50,7 @@ struct UpK {
   const float* scale; const float* bias; const float* slope; int act;
   int per_row;    // Wo * (Co / VW)
   int chunks;     // ceil(per_row / 256)
+  int y_planes;   // write y in the planes format (include/prpe.h, prpe_conv_desc)
 };
 
 // Fused one-pass form (no workspace). One thread = VW channels of one output column, for a
@@ -137,6 +138,20 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
     for (int v = 0; v < VW; ++v) out[v] = apply_act(acc[v] * sc[v] + bi[v], p.act, sl[v]);
     float* y = yp + (int64_t)oy * p.y.sh;
     if constexpr (VW == 4) {
+      if (p.y_planes) {
+        // channel group c0 / 8 of the pixel: hi[8] then lo[8] (bf16 RNE two-plane split)
+        uint16_t* y16 = reinterpret_cast<uint16_t*>(y - c0) + (c0 >> 3) * 16 + (c0 & 7);
+        unsigned short hi[4], lo[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          const __bf16 h = (__bf16)out[v];
+          hi[v] = __builtin_bit_cast(unsigned short, h);
+          lo[v] = __builtin_bit_cast(unsigned short, (__bf16)(out[v] - (float)h));
+        }
+        *reinterpret_cast<uint2*>(y16) = make_uint2(hi[0] | (unsigned)hi[1] << 16, hi[2] | (unsigned)hi[3] << 16);
+        *reinterpret_cast<uint2*>(y16 + 8) = make_uint2(lo[0] | (unsigned)lo[1] << 16, lo[2] | (unsigned)lo[3] << 16);
+        continue;
+      }
       if (p.y.sc == 1) {
         *reinterpret_cast<float4*>(y) = make_float4(out[0], out[1], out[2], out[3]);
         continue;
@@ -525,12 +540,13 @@ extern "C" int64_t prpe_upconv3x3_workspace_bytes(const prpe_view* z, const prpe
 
 extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,
                               const float* scale, const float* bias, const float* slope, int32_t act,
-                              void* workspace, int64_t workspace_bytes, void* stream) {
+                              int32_t y_planes, void* workspace, int64_t workspace_bytes, void* stream) {
   if (!view_ok(z) || !view_ok(y) || z->n != y->n || z->c != 9 * y->c) return PRPE_EINVAL;
   if (act == PRPE_ACT_PRELU && !slope) return PRPE_EINVAL;
   UpK p{};
   p.z = *z; p.y = *y; p.Co = y->c; p.ac = align_corners ? 1 : 0;
   p.scale = scale; p.bias = bias; p.slope = slope; p.act = act;
+  p.y_planes = y_planes ? 1 : 0;
   const bool v4 = (y->c % 4 == 0) && z->sc == 1 && (z->sw % 4 == 0) && (z->sh % 4 == 0) &&
                   (z->sn % 4 == 0) && ((uintptr_t)z->ptr % 16 == 0) &&
                   (y->sc != 1 || ((y->sw % 4 == 0) && (y->sh % 4 == 0) && (y->sn % 4 == 0) &&
@@ -543,6 +559,9 @@ extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t al
       !rowgrid((int64_t)y->n * 3 * z->h, p.per_row, g_h, p.chunks))
     return PRPE_EINVAL;
   const int64_t need = prpe_upconv3x3_workspace_bytes(z, y);
+  if (y_planes && (!v4 || y->sc != 1 || y->c % 8 || y->sw % 8 || y->sh % 8 || y->sn % 8 ||
+                   (uintptr_t)y->ptr % 32 || workspace))
+    return PRPE_EINVAL;
   if (workspace && workspace_bytes >= need && ((uintptr_t)workspace % 16) == 0) {
     float* H = static_cast<float*>(workspace);
     if (v4) {

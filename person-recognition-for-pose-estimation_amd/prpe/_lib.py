@@ -35,7 +35,7 @@ class ConvDesc(C.Structure):
                 ("k_order", C.c_int32),
                 ("w_h16", C.c_void_p), ("w_l16", C.c_void_p), ("scale16", C.c_void_p),
                 ("x_amax", C.c_void_p), ("y_amax", C.c_void_p),
-                ("x2", View), ("x2_amax", C.c_void_p)]
+                ("x2", View), ("x2_amax", C.c_void_p), ("x_planes", C.c_int32), ("y_planes", C.c_int32)]
 
 
 ACT = {"none": 0, "relu": 1, "silu": 2, "prelu": 3, "gelu": 4, "sigmoid": 5}
@@ -50,7 +50,7 @@ _VP = C.POINTER(View)
 SIGNATURES = {
     "prpe_conv2d": (C.c_int, [C.POINTER(ConvDesc), _P]),
     "prpe_upconv3x3_workspace_bytes": (C.c_int64, [_VP, _VP]),
-    "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _P, _L, _P]),
+    "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _I, _P, _L, _P]),
     "prpe_dwconv": (C.c_int, [_VP, _VP, _VP, _P, _I, _I, _I, _P, _P, _I, _P]),
     "prpe_maxpool": (C.c_int, [_VP, _VP, _I, _I, _I, _P]),
     "prpe_upsample_nearest2x": (C.c_int, [_VP, _VP, _P]),

@@ -17,6 +17,8 @@ Reference structure mirrored function by function (see prpe.arch for citations).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import arch, ops
@@ -37,6 +39,8 @@ BN_EPS = 1e-5
 # split.
 AUTO_POLICY = {"trunk": 3, "yolo_adapter": 0, "yolo_net": 2, "adaface": 0, "vit": 0}
 AMAX_SLOTS = 4096
+# PRPE_PLANES=0 keeps every activation in fp32 (A/B runs of the planes-format handoff)
+PLANES_ON = os.environ.get("PRPE_PLANES", "1") != "0"
 
 
 class _Prec:
@@ -145,8 +149,10 @@ class Engine:
             self._packs[name] = p
         return p
 
-    def conv(self, x, p: ConvPack, out=None, res=None, res_mode=0, act=None, x2=None, x2_amax=None):
-        """``x2``: second 1x1 input on the output grid (dual-input GEMM, see prpe.h)."""
+    def conv(self, x, p: ConvPack, out=None, res=None, res_mode=0, act=None, x2=None, x2_amax=None,
+             planes_out=False):
+        """``x2``: second 1x1 input on the output grid (dual-input GEMM, see prpe.h).
+        ``planes_out``: the only consumer is a precision-0 wave-row conv: write the planes format."""
         B, H, W, _ = x.shape
         Ho = (H + 2 * p.pad - p.kh) // p.stride + 1
         Wo = (W + 2 * p.pad - p.kw) // p.stride + 1
@@ -157,8 +163,12 @@ class Engine:
             prec = 2
         xa = getattr(x, "_prpe_amax", None) if prec == 3 else None
         ya = self.amax_slot() if self.precision == 3 else None
+        x_planes = getattr(x, "_prpe_planes", False)
+        if x_planes and prec != 0:
+            raise RuntimeError(f"{p.name}: planes-format input needs precision 0, got {prec}")
+        y_planes = PLANES_ON and planes_out and prec == 0 and p.co % 8 == 0 and out.is_contiguous()
         kw = dict(res=res, res_mode=res_mode, act=act, precision=prec, x_amax=xa, y_amax=ya, x2=x2,
-                  x2_amax=x2_amax if prec == 3 else None)
+                  x2_amax=x2_amax if prec == 3 else None, x_planes=x_planes, y_planes=y_planes)
         if p.name in self.watch:          # HIP events around one kernel (bench roofline)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -168,10 +178,15 @@ class Engine:
         else:
             ops.conv2d(x, p, out, **kw)
         out._prpe_amax = ya
+        if y_planes:
+            out._prpe_planes = True
         return out
 
-    def upconv(self, name, x, wkey, size, align_corners, bn=None, bias_key=None, act="none", prelu=None, out=None):
-        """conv3x3(pad 1)(bilinear_upsample(x, size)) [+BN] [+act] via the tap rewrite."""
+    def upconv(self, name, x, wkey, size, align_corners, bn=None, bias_key=None, act="none", prelu=None, out=None,
+               planes=False):
+        """conv3x3(pad 1)(bilinear_upsample(x, size)) [+BN] [+act] via the tap rewrite.
+        ``planes``: the only consumer is a precision-0 conv, so write the planes format (the
+        consumer's two-plane split done once here; include/prpe.h)."""
         taps = self._packs.get(name + ":taps")
         if taps is None:
             taps = pack_upconv_taps(name + ":taps", self.sd[wkey], self.device)
@@ -191,7 +206,11 @@ class Engine:
         if out is None:
             out = self.empty(B, size[0], size[1], co)
         slope = self.dev(prelu) if prelu else None
-        return ops.upconv3x3(z, out, align_corners, self._aux[key], self._aux[key + "b"], slope, act)
+        planes = PLANES_ON and planes and self.precision == 0 and co % 8 == 0 and out.is_contiguous()
+        ops.upconv3x3(z, out, align_corners, self._aux[key], self._aux[key + "b"], slope, act, y_planes=planes)
+        if planes:
+            out._prpe_planes = True
+        return out
 
     # ------------------------------------------------------------------ ResNet-50 trunk
     def trunk(self, x_nchw, flip_w=False):
@@ -338,8 +357,9 @@ class Engine:
         a = p + ".adapter"
         t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="silu"))
         u = self.upconv(a + ".4", t, a + ".4.weight", (160, 160), True, bn=a + ".5", bias_key=a + ".4.bias",
-                        act="silu")
-        t = self.conv(u, self.pk(a + ".7", a + ".7.weight", bn=a + ".8", bias_key=a + ".7.bias", act="silu"))
+                        act="silu", planes=True)
+        t = self.conv(u, self.pk(a + ".7", a + ".7.weight", bn=a + ".8", bias_key=a + ".7.bias", act="silu"),
+                      planes_out=True)
         t = self.conv(t, self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias",
                                  act="silu"))
         t = self.conv(t, self.pk(a + ".13", a + ".13.weight", bn=a + ".14", bias_key=a + ".13.bias", act="silu"))
@@ -412,7 +432,7 @@ class Engine:
         t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="prelu",
                                     prelu=a + ".2.weight"))
         u = self.upconv(a + ".4", t, a + ".4.weight", (112, 112), True, bn=a + ".5", bias_key=a + ".4.bias",
-                        act="prelu", prelu=a + ".6.weight")
+                        act="prelu", prelu=a + ".6.weight", planes=True)
         t = self.conv(u, self.pk(a + ".7", a + ".7.weight", 1, 1, bn=a + ".8", bias_key=a + ".7.bias", act="prelu",
                                  prelu=a + ".9.weight"))
         t = self.conv(t, self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias",
@@ -453,7 +473,7 @@ class Engine:
         a = "vit_pose.adapter"
         t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="gelu"))
         u = self.upconv(a + ".4", t, a + ".4.weight", arch.VIT_IMG, True, bn=a + ".5", bias_key=a + ".4.bias",
-                        act="gelu")
+                        act="gelu", planes=True)
         t = self.conv(u, self.pk(a + ".7", a + ".7.weight", 1, 1, bn=a + ".8", bias_key=a + ".7.bias", act="gelu"))
         return self.conv(t, self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias",
                                     act="gelu"))
@@ -496,7 +516,8 @@ class Engine:
                            res=as4(X2), res_mode=RES_PRE).view(B * L, D)
             hn = ops.layernorm(X2, self.empty(B * L, D), self.dev(q + ".layernorm_after.weight"),
                                self.dev(q + ".layernorm_after.bias"))
-            f1 = self.conv(as4(hn), self._lin(q + ":fc1", q + ".mlp.fc1.weight", q + ".mlp.fc1.bias", act="gelu"))
+            f1 = self.conv(as4(hn), self._lin(q + ":fc1", q + ".mlp.fc1.weight", q + ".mlp.fc1.bias", act="gelu"),
+                           planes_out=True)
             X2 = self.conv(f1, self._lin(q + ":fc2", q + ".mlp.fc2.weight", q + ".mlp.fc2.bias"),
                            res=as4(X2), res_mode=RES_PRE).view(B * L, D)
         hn = ops.layernorm(X2, self.empty(B * L, D), self.dev(v + ".layernorm.weight"), self.dev(v + ".layernorm.bias"),

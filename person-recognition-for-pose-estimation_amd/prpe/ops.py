@@ -37,7 +37,7 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
 
 
 def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, tile=0, x_amax=None,
-           y_amax=None, x2=None, x2_amax=None):
+           y_amax=None, x2=None, x2_amax=None, x_planes=False, y_planes=False):
     """y = EPI(conv(PRO(x))) with a ``ConvPack`` (see prpe.pack).
 
     precision 3 (split fp16) needs ``x_amax``: a 1-element device tensor bounding max|x| (e.g.
@@ -49,6 +49,7 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
         d.w_h16, d.w_l16, d.scale16 = h16.data_ptr(), l16.data_ptr(), s16.data_ptr()
         d.x_amax = _ptr(x_amax)
     d.y_amax = _ptr(y_amax)
+    d.x_planes, d.y_planes = int(x_planes), int(y_planes)   # planes format, see prpe.h
     if x2 is not None:                 # second 1x1 input, see prpe.h (dual input)
         d.x2 = view(x2)
         d.x2_amax = _ptr(x2_amax)
@@ -69,7 +70,8 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
     return y
 
 
-def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none", separable=False):
+def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none", separable=False,
+              y_planes=False):
     """Fused one-pass kernel by default; ``separable=True`` runs the two-pass workspace form."""
     zv, yv = view(z), view(y)
     ws, nbytes = None, 0
@@ -77,7 +79,7 @@ def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none"
         nbytes = lib().prpe_upconv3x3_workspace_bytes(C.byref(zv), C.byref(yv))
         ws = torch.empty((nbytes + 3) // 4, device=z.device, dtype=torch.float32)
     check(lib().prpe_upconv3x3(C.byref(zv), C.byref(yv), 1 if align_corners else 0, _ptr(scale), _ptr(bias),
-                               _ptr(slope), ACT[act], _ptr(ws), nbytes, _stream()), "prpe_upconv3x3")
+                               _ptr(slope), ACT[act], int(y_planes), _ptr(ws), nbytes, _stream()), "prpe_upconv3x3")
     return y
 
 

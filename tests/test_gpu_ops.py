@@ -423,6 +423,70 @@ def test_conv_dual_input_rejects_bad_geometry():
                    x2=torch.zeros(1, 5, 5, 16, device=DEV))
 
 
+def _decode_planes(t):
+    """planes format -> (hi, lo) fp32 tensors of the logical shape [N,H,W,C]."""
+    n, h, w, c = t.shape
+    u = t.contiguous().view(torch.int16).view(n, h, w, c // 8, 2, 8)
+    hi = u[..., 0, :].contiguous().view(torch.bfloat16).float().reshape(n, h, w, c)
+    lo = u[..., 1, :].contiguous().view(torch.bfloat16).float().reshape(n, h, w, c)
+    return hi, lo
+
+
+@pytest.mark.parametrize("k1,k2", [(1, 3), (3, 1), (3, 3)])
+def test_planes_format_producer_consumer_bit_exact(k1, k2):
+    """A conv writing the planes format + a precision-0 conv reading it == the fp32 tensor +
+    the consumer's own split, bit for bit; the format holds hi = RNE(v), lo = RNE(v - hi)."""
+    x = rnd(2, 64, 13, 11, seed=121).permute(0, 2, 3, 1).contiguous().to(DEV)
+    w1 = rnd(128, 64, k1, k1, seed=122, scale=0.05)
+    w2 = rnd(96, 128, k2, k2, seed=123, scale=0.03)
+    p1 = pack.pack_conv("a", w1, 1, k1 // 2, DEV, act="silu")
+    p2 = pack.pack_conv("b", w2, 1, k2 // 2, DEV, act="gelu")
+    t32 = torch.empty(2, 13, 11, 128, device=DEV)
+    tpl = torch.empty(2, 13, 11, 128, device=DEV)
+    ops.conv2d(x, p1, t32, precision=0)
+    ops.conv2d(x, p1, tpl, precision=0, y_planes=True)
+    y32 = torch.empty(2, 13, 11, 96, device=DEV)
+    ypl = torch.empty(2, 13, 11, 96, device=DEV)
+    ops.conv2d(t32, p2, y32, precision=0, tile=26)
+    ops.conv2d(tpl, p2, ypl, precision=0, x_planes=True)
+    torch.cuda.synchronize()
+    hi, lo = _decode_planes(tpl.cpu())
+    v = t32.cpu()
+    assert torch.equal(hi, v.to(torch.bfloat16).float())
+    assert torch.equal(lo, (v - hi).to(torch.bfloat16).float())
+    assert torch.equal(y32.cpu(), ypl.cpu())
+
+
+@pytest.mark.parametrize("hi_,wi,ho,wo,act", [(20, 20, 160, 160, "silu"), (20, 20, 256, 192, "gelu")])
+def test_upconv_planes_output_feeds_conv_bit_exact(hi_, wi, ho, wo, act):
+    co = 64
+    z = rnd(2, hi_, wi, 9 * co, seed=124).to(DEV)
+    sc = (torch.rand(co, generator=_g(125)) + 0.5).to(DEV)
+    bi = rnd(co, seed=126).to(DEV)
+    u32 = torch.empty(2, ho, wo, co, device=DEV)
+    upl = torch.empty(2, ho, wo, co, device=DEV)
+    ops.upconv3x3(z, u32, True, sc, bi, None, act)
+    ops.upconv3x3(z, upl, True, sc, bi, None, act, y_planes=True)
+    w = rnd(128, co, 3, 3, seed=127, scale=0.05)
+    pk = pack.pack_conv("c", w, 1, 1, DEV)
+    y32 = torch.empty(2, ho, wo, 128, device=DEV)
+    ypl = torch.empty(2, ho, wo, 128, device=DEV)
+    ops.conv2d(u32, pk, y32, precision=0, tile=26)
+    ops.conv2d(upl, pk, ypl, precision=0, x_planes=True)
+    torch.cuda.synchronize()
+    hi, lo = _decode_planes(upl.cpu())
+    assert torch.equal(hi, u32.cpu().to(torch.bfloat16).float())
+    assert torch.equal(y32.cpu(), ypl.cpu())
+
+
+def test_planes_format_rejected_outside_precision_0():
+    x = rnd(1, 64, 5, 5, seed=128).permute(0, 2, 3, 1).contiguous().to(DEV)
+    pk = pack.pack_conv("t", rnd(64, 64, 1, 1, seed=129), 1, 0, DEV)
+    y = torch.empty(1, 5, 5, 64, device=DEV)
+    with pytest.raises(PrpeError):
+        ops.conv2d(x, pk, y, precision=2, x_planes=True)
+
+
 def test_conv_y_amax_every_kernel_family():
     """y_amax from the register-staged (scalar and vector epilogues), LDS-DMA and wave-row
     kernels and the small-Co kernel."""
