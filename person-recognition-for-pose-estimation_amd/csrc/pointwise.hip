@@ -9,6 +9,7 @@
 //   l2norm        : row L2 normalisation
 //   dfl_decode    : YOLO head eval decode (DFL softmax-expectation, anchors, strides, sigmoid)
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -574,7 +575,14 @@ extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t al
     return launch_status();
   }
   // fused path: R output rows per thread; shrink R while the grid would not fill the chip
-  int R = 32;
+  // rows per thread: each thread's first rows rebuild both interpolation rows of every dy, so
+  // long runs amortise that (measured, tools/upconv_bench.py bs=256: R 32 -> 256 = +4..10 %);
+  // PRPE_UPCONV_R overrides it for A/B runs
+  static const int r_env = [] {
+    const char* e = getenv("PRPE_UPCONV_R");
+    return e ? atoi(e) : 256;
+  }();
+  int R = r_env;
   while (R > 4 && (int64_t)y->n * ((y->h + R - 1) / R) * p.chunks < 8192) R /= 2;
   const int rblocks = (y->h + R - 1) / R;
   const int64_t nb = (int64_t)y->n * rblocks * p.chunks;
