@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PRPE_ABI_VERSION 2
+#define PRPE_ABI_VERSION 3
 
 /* activations (epilogues/prologues) */
 enum prpe_act {
@@ -134,8 +134,8 @@ int prpe_conv2d(const prpe_conv_desc* d, void* stream);
  * source rows are kept in rolling registers, HBM traffic = y write + z read. With a workspace
  * of >= prpe_upconv3x3_workspace_bytes(z, y) bytes the sum is instead evaluated in two passes
  * through it (x-interpolation, then y; kept for ablation). Both agree to fp32 rounding.
- * y_planes: write y in the planes format of prpe_conv_desc (fused path, C % 8 == 0,
- * channel-contiguous, 32-B aligned) for a precision-0 consumer conv.
+ * y_planes: write y in the planes format described at prpe_conv_desc: fused path, C % 8 == 0,
+ * channel-contiguous, 32-B aligned; for a precision-0 consumer conv.
  */
 int64_t prpe_upconv3x3_workspace_bytes(const prpe_view* z, const prpe_view* y);
 int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,
