@@ -242,6 +242,30 @@ int prpe_flip_average(const float* heat, const float* heat_flipped, float* out, 
 int prpe_ce_argmax(const float* logits, int64_t ld, int32_t B, int32_t C, const int64_t* labels,
                    float* loss, int32_t* argmax, float* summary, void* stream);
 
+/*
+ * Detection eval metrics (DetectionMetrics, training/lightning/face_detection/module_v2.py:13-127,
+ * as driven by validation_step :458-499). State is caller-allocated on
+ * the device: counters uint64 [4] = (tp, fp, gt, records), zeroed to reset; records float
+ * [capacity][2] = (score, best IoU) appended in image, then prediction order.
+ * update: dets [B, max_det, 6] (x1,y1,x2,y2,conf,cls) + counts [B] from prpe_nms, ground truth
+ * gt_boxes [G, 4] xyxy with gt_batch [G] (int64 image index, the reference's targets['batch_idx']);
+ * images with no prediction or no ground truth are skipped (validation_step's `continue`s);
+ * each prediction's best IoU over its image's boxes (box_iou: inter / (union + 1e-6), fp32),
+ * tp if > 0.5. Records past capacity are dropped (counters[3] still counts them).
+ * compute (epoch end): n = counters[3] (host value), thresholds = host float[10]
+ * (torch.linspace(0.5, 0.95, 10)); out double[6] = precision, recall, f1, mAP50, mAP75, mAP
+ * (compute(): stable descending sort by score, per-threshold cumulative tp/fp, torch.trapz).
+ */
+int64_t prpe_det_metrics_update_workspace_bytes(int32_t B);
+int prpe_det_metrics_update(const float* dets, const int32_t* counts, int32_t B, int32_t max_det,
+                            const float* gt_boxes, const int64_t* gt_batch, int32_t G, uint64_t* counters,
+                            float* records, int64_t capacity, void* workspace, int64_t workspace_bytes,
+                            void* stream);
+int64_t prpe_det_metrics_compute_workspace_bytes(int64_t n);
+int prpe_det_metrics_compute(const uint64_t* counters, const float* records, int64_t n,
+                             const float* thresholds, double* out, void* workspace, int64_t workspace_bytes,
+                             void* stream);
+
 /* ABI version / build info. */
 int prpe_abi_version(void);
 const char* prpe_build_info(void);

@@ -417,3 +417,57 @@ def face_recognition_eval(embeddings: Tensor, head_kernel: Tensor, labels: Tenso
     amax = output.max(1)[1]
     acc = (amax == labels).float().mean()
     return loss, acc, output, amax
+
+
+class DetectionMetricsRef:
+    """DetectionMetrics (training/lightning/face_detection/module_v2.py:13-127) restated, as
+    driven by FaceDetectionModule.validation_step (:480-499): test infrastructure only."""
+
+    def __init__(self):
+        self.tp = self.fp = self.gt = 0
+        self.records = []                      # (score, is_tp, iou), insertion order
+
+    @staticmethod
+    def box_iou(b1: Tensor, b2: Tensor) -> Tensor:                    # :27-45
+        a1 = (b1[:, 2] - b1[:, 0]) * (b1[:, 3] - b1[:, 1])
+        a2 = (b2[:, 2] - b2[:, 0]) * (b2[:, 3] - b2[:, 1])
+        lt = torch.max(b1[:, None, :2], b2[:, :2])
+        rb = torch.min(b1[:, None, 2:], b2[:, 2:])
+        wh = (rb - lt).clamp(min=0)
+        inter = wh[:, :, 0] * wh[:, :, 1]
+        union = a1[:, None] + a2 - inter
+        return inter / (union + 1e-6)
+
+    def update_batch(self, preds: list, gt_boxes: Tensor, batch_idx: Tensor):   # :480-499 + :47-78
+        for i, pred in enumerate(preds):
+            if len(pred) == 0:
+                continue
+            g = gt_boxes[batch_idx == i]
+            if len(g) == 0:
+                continue
+            best = self.box_iou(pred[:, :4], g).max(dim=1)[0]
+            for s, v in zip(pred[:, 4].tolist(), best.tolist()):
+                t = v > 0.5
+                self.tp += int(t)
+                self.fp += int(not t)
+                self.records.append((s, t, v))
+            self.gt += len(g)
+
+    def compute(self) -> dict:                                          # :80-127
+        precision = self.tp / (self.tp + self.fp + 1e-6)
+        recall = self.tp / (self.gt + 1e-6)
+        f1 = 2 * (precision * recall) / (precision + recall + 1e-6)
+        aps = []
+        for thr in torch.linspace(0.5, 0.95, 10):
+            kept = [r for r in self.records if r[2] >= thr]
+            if not kept:
+                aps.append(0.0)
+                continue
+            kept = sorted(kept, key=lambda x: x[0], reverse=True)
+            tp = torch.tensor([x[1] for x in kept])
+            tpc, fpc = torch.cumsum(tp, 0), torch.cumsum(~tp, 0)
+            rec = torch.cat((torch.tensor([0]), tpc / (self.gt + 1e-6), torch.tensor([1])))
+            prec = torch.cat((torch.tensor([1]), tpc / (tpc + fpc + 1e-6), torch.tensor([0])))
+            aps.append(torch.trapz(prec, rec).item())
+        return {"precision": precision, "recall": recall, "f1": f1, "mAP50": aps[0], "mAP75": aps[5],
+                "mAP": sum(aps) / len(aps)}

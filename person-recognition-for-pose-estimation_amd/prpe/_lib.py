@@ -66,6 +66,10 @@ SIGNATURES = {
     "prpe_softargmax": (C.c_int, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),
     "prpe_flip_average": (C.c_int, [_P, _P, _P, _I, _I, _I, _I, C.POINTER(C.c_int32), _I, _P]),
     "prpe_ce_argmax": (C.c_int, [_P, _L, _I, _I, _P, _P, _P, _P, _P]),
+    "prpe_det_metrics_update_workspace_bytes": (C.c_int64, [_I]),
+    "prpe_det_metrics_update": (C.c_int, [_P, _P, _I, _I, _P, _P, _I, _P, _P, _L, _P, _L, _P]),
+    "prpe_det_metrics_compute_workspace_bytes": (C.c_int64, [_L]),
+    "prpe_det_metrics_compute": (C.c_int, [_P, _P, _L, _P, _P, _P, _L, _P]),
     "prpe_abi_version": (C.c_int, []),
     "prpe_build_info": (C.c_char_p, []),
 }

@@ -12,6 +12,11 @@
   [B,512] x [512,classes] cosine GEMM with the scale s folded into the epilogue (prpe_conv2d,
   fp32-faithful 3-plane mode), and cross-entropy + argmax + accuracy on device
   (prpe_ce_argmax).
+* ``DetectionMetricsDevice`` — the detection validation step's DetectionMetrics
+  (training/lightning/face_detection/module_v2.py:13-127, driven by validation_step :458-499):
+  per batch one launch matches the padded NMS output against the ground truth and appends
+  (score, best IoU) records on device (prpe_det_metrics_update); compute() at epoch end
+  (prpe_det_metrics_compute) returns the reference's dict.
 """
 from __future__ import annotations
 
@@ -84,3 +89,29 @@ class FaceRecognitionEval:
         if labels is None:
             return None, None, amax
         return summary[0], summary[1], amax
+
+
+class DetectionMetricsDevice:
+    """DetectionMetrics with its state on the device (same update/compute semantics)."""
+
+    THRESHOLDS = torch.linspace(0.5, 0.95, 10).tolist()     # module_v2.py:92
+    KEYS = ("precision", "recall", "f1", "mAP50", "mAP75", "mAP")
+
+    def __init__(self, device="cuda", capacity: int = 1 << 20):
+        self.counters = torch.zeros(4, dtype=torch.int64, device=device)   # tp, fp, gt, records
+        self.records = torch.empty(capacity, 2, dtype=torch.float32, device=device)
+
+    def reset(self):
+        self.counters.zero_()
+
+    def update_batch(self, dets, counts, gt_boxes, gt_batch):
+        """dets [B, max_det, 6] + counts [B] (postproc.non_max_suppression_padded); gt_boxes [G, 4]
+        xyxy with gt_batch [G] = the reference's targets['boxes'] / targets['batch_idx']."""
+        ops.det_metrics_update(dets, counts, gt_boxes, gt_batch, self.counters, self.records)
+
+    def compute(self) -> dict:
+        n = int(self.counters[3].item())          # one host read per epoch
+        if n > self.records.shape[0]:
+            raise RuntimeError(f"DetectionMetricsDevice: {n} records exceed the capacity {self.records.shape[0]}")
+        out = ops.det_metrics_compute(self.counters, self.records, n, self.THRESHOLDS).tolist()
+        return dict(zip(self.KEYS, out))

@@ -201,3 +201,27 @@ def ce_argmax(logits, labels=None):
     check(lib().prpe_ce_argmax(logits.data_ptr(), logits.stride(0), B, Cn, _ptr(labels), _ptr(loss), amax.data_ptr(),
                                _ptr(summary), _stream()), "prpe_ce_argmax")
     return loss, amax, summary
+
+
+def det_metrics_update(dets, counts, gt_boxes, gt_batch, counters, records):
+    """Append one batch to the device DetectionMetrics state (see include/prpe.h)."""
+    B, max_det, six = dets.shape
+    assert six == 6 and dets.is_contiguous() and counts.dtype == torch.int32
+    gt = gt_boxes.to(device=dets.device, dtype=torch.float32).contiguous().view(-1, 4)
+    gb = gt_batch.to(device=dets.device, dtype=torch.int64).contiguous().view(-1)
+    nbytes = lib().prpe_det_metrics_update_workspace_bytes(B)
+    ws = torch.empty(max(1, (nbytes + 3) // 4), device=dets.device, dtype=torch.float32)
+    check(lib().prpe_det_metrics_update(dets.data_ptr(), counts.contiguous().data_ptr(), B, max_det, gt.data_ptr(),
+                                        gb.data_ptr(), gt.shape[0], counters.data_ptr(), records.data_ptr(),
+                                        records.shape[0], ws.data_ptr(), nbytes, _stream()), "prpe_det_metrics_update")
+
+
+def det_metrics_compute(counters, records, n, thresholds):
+    """(precision, recall, f1, mAP50, mAP75, mAP) as a float64 device tensor [6]."""
+    nbytes = lib().prpe_det_metrics_compute_workspace_bytes(n)
+    ws = torch.empty((nbytes + 3) // 4, device=counters.device, dtype=torch.float32)
+    out = torch.empty(6, device=counters.device, dtype=torch.float64)
+    thr = (C.c_float * len(thresholds))(*[float(t) for t in thresholds])
+    check(lib().prpe_det_metrics_compute(counters.data_ptr(), records.data_ptr(), n, C.cast(thr, C.c_void_p),
+                                         out.data_ptr(), ws.data_ptr(), nbytes, _stream()), "prpe_det_metrics_compute")
+    return out

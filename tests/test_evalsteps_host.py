@@ -29,3 +29,31 @@ def test_reference_flip_pairs_reverse_the_batch():
     for k in range(K):
         k2 = part[k] if part[k] >= 0 else k
         assert torch.equal(swap[:, k], torch.flip(f[:, k2], dims=[-1]))
+
+
+def _golden_detmetrics():
+    import os
+    import numpy as np
+    return dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_detmetrics.npz")))
+
+
+def test_detection_metrics_oracle_matches_reference_golden():
+    """oracle.DetectionMetricsRef == the reference's DetectionMetrics (module_v2.py:13-127) as
+    driven by validation_step, on the fixtures it produced (oracle/make_golden_detmetrics.py):
+    counters, (score, is_tp, iou) records in order, and every compute() value."""
+    g = _golden_detmetrics()
+    m = R.DetectionMetricsRef()
+    for b in range(2):
+        dets, counts = torch.from_numpy(g[f"dets{b}"]), torch.from_numpy(g[f"counts{b}"])
+        preds = [dets[i, :int(counts[i])] for i in range(dets.shape[0])]
+        m.update_batch(preds, torch.from_numpy(g[f"gt{b}"]), torch.from_numpy(g[f"gtidx{b}"]))
+    assert [m.tp, m.fp, m.gt, len(m.records)] == g["counters"].tolist()
+    rec = torch.tensor([[s, float(t), v] for s, t, v in m.records], dtype=torch.float64)
+    assert torch.equal(rec, torch.from_numpy(g["records"]))
+    out = m.compute()
+    got = [out[k] for k in ("precision", "recall", "f1", "mAP50", "mAP75", "mAP")]
+    assert got == g["metrics"].tolist()
+    # the fixture covers the reference's edge cases
+    assert any(r[2] == 0.5 for r in m.records)                       # IoU exactly 0.5: not a TP
+    scores = [r[0] for r in m.records]
+    assert len(set(scores)) < len(scores)                            # tied scores

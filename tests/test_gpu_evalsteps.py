@@ -97,3 +97,65 @@ def test_face_recognition_eval_vs_oracle(model):
     assert abs(loss.item() - rl.item()) <= 1e-4 * max(1.0, abs(rl.item()))
     if not torch.any(near_tie):
         assert acc.item() == racc.item()
+
+
+def _golden_detmetrics():
+    import os
+    import numpy as np
+    return dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_detmetrics.npz")))
+
+
+def test_detection_metrics_device_vs_reference_golden():
+    """Device DetectionMetrics on the reference's own fixtures: counters and records exact
+    (IoUs bit-exact), precision/recall/f1 exact, APs to fp32 summation order (1e-6)."""
+    from prpe.evalsteps import DetectionMetricsDevice
+    g = _golden_detmetrics()
+    m = DetectionMetricsDevice("cuda", capacity=4096)
+    for b in range(2):
+        m.update_batch(torch.from_numpy(g[f"dets{b}"]).cuda(), torch.from_numpy(g[f"counts{b}"]).cuda(),
+                       torch.from_numpy(g[f"gt{b}"]).cuda(), torch.from_numpy(g[f"gtidx{b}"]).cuda())
+    torch.cuda.synchronize()
+    assert m.counters.cpu().tolist() == g["counters"].tolist()
+    n = int(g["counters"][3])
+    rec = m.records[:n].cpu().double()
+    ref = torch.from_numpy(g["records"])
+    assert torch.equal(rec[:, 0], ref[:, 0]) and torch.equal(rec[:, 1], ref[:, 2])
+    out = m.compute()
+    keys = ("precision", "recall", "f1", "mAP50", "mAP75", "mAP")
+    for k, v in zip(keys, g["metrics"].tolist()):
+        if k in ("precision", "recall", "f1"):
+            assert out[k] == v, k
+        else:
+            assert abs(out[k] - v) <= 1e-6 * max(1.0, abs(v)), (k, out[k], v)
+    m.reset()
+    assert all(v == 0.0 for v in m.compute().values())
+
+
+def test_detection_metrics_device_large_vs_oracle():
+    """Many batches (records span several 2048-record scan tiles), the oracle as reference."""
+    from oracle import model_ref as R
+    from prpe.evalsteps import DetectionMetricsDevice
+    gen = torch.Generator().manual_seed(5)
+    m = DetectionMetricsDevice("cuda", capacity=1 << 16)
+    ref = R.DetectionMetricsRef()
+    for _ in range(6):
+        B, cap = 16, 300
+        dets = torch.zeros(B, cap, 6)
+        counts = torch.randint(0, cap + 1, (B,), generator=gen, dtype=torch.int32)
+        ng = torch.randint(0, 6, (B,), generator=gen)
+        gt = torch.cat([torch.cat([c := torch.rand(int(k), 2, generator=gen) * 400,
+                                   c + torch.rand(int(k), 2, generator=gen) * 80 + 5], 1) for k in ng])
+        gidx = torch.repeat_interleave(torch.arange(B), ng)
+        for i in range(B):
+            n = int(counts[i])
+            sc = torch.sort(torch.round(torch.rand(n, generator=gen) * 50) / 50, descending=True, stable=True)[0]
+            c = torch.rand(n, 2, generator=gen) * 400
+            dets[i, :n, :2], dets[i, :n, 2:4] = c, c + torch.rand(n, 2, generator=gen) * 80 + 5
+            dets[i, :n, 4] = sc
+        m.update_batch(dets.cuda(), counts.cuda(), gt.cuda(), gidx.cuda())
+        ref.update_batch([dets[i, :int(counts[i])] for i in range(B)], gt, gidx)
+    assert m.counters.cpu().tolist() == [ref.tp, ref.fp, ref.gt, len(ref.records)]
+    assert len(ref.records) > 3 * 2048
+    out, exp = m.compute(), ref.compute()
+    for k in exp:
+        assert abs(out[k] - exp[k]) <= 1e-5 * max(1.0, abs(exp[k])), (k, out[k], exp[k])
