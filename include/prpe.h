@@ -266,6 +266,18 @@ int prpe_det_metrics_compute(const uint64_t* counters, const float* records, int
                              const float* thresholds, double* out, void* workspace, int64_t workspace_bytes,
                              void* stream);
 
+/*
+ * Detection eval loss (FaceDetectionModule.compute_loss, module_v2.py:178-303, as validation_step
+ * :467 calls it on the eval head output): boxes [B, 4, N] and scores [B, C, N] as strided views
+ * (element strides [3] each, host arrays), ground truth gt_boxes [G, 4] / gt_batch [G] / optional
+ * gt_classes [G] (int64). per_image [B][4] = (loss_b, box, cls, bg) (NaN where the reference
+ * computes no such term), loss [1] = sum_b loss_b / B. N <= 1024. See csrc/detmetrics.hip.
+ */
+int prpe_det_eval_loss(const float* boxes, const int64_t* box_strides, const float* scores,
+                       const int64_t* score_strides, int32_t B, int32_t C, int32_t N, const float* gt_boxes,
+                       const int64_t* gt_batch, const int64_t* gt_classes, int32_t G, float* per_image,
+                       float* loss, void* stream);
+
 /* ABI version / build info. */
 int prpe_abi_version(void);
 const char* prpe_build_info(void);

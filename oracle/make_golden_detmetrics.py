@@ -1,8 +1,9 @@
 """Golden fixtures for the device DetectionMetrics, made by the
-reference's OWN class in this container (import shims as in make_golden.py; test
+reference's OWN classes in this container (import shims as in make_golden.py; test
 infrastructure only, never shipped to the GPU box):
 
-    python -B oracle/make_golden_detmetrics.py   ->  tests/golden/golden_detmetrics.npz
+    python -B oracle/make_golden_detmetrics.py   ->  tests/golden/golden_detmetrics.npz,
+                                                    tests/golden/golden_detloss.npz
 
 Inputs: two synthetic batches of padded NMS outputs [B, 300, 6] + counts and ground-truth
 boxes with batch indices, with the edge cases the reference code distinguishes: images with
@@ -61,9 +62,65 @@ def make_batch(seed, B=6, cap=300):
     return dets, counts, torch.cat(gts, 0), torch.tensor(gidx, dtype=torch.int64)
 
 
+def loss_inputs(seed=21, B=6, N=525):
+    """Eval head output [B, 5, N] (boxes taken as xyxy, as compute_loss does; scores in (0, 1))
+    with per-image cases: positives and negatives, no ground truth, nothing above 0.01, kept
+    predictions but no positive, many positives with a single negative."""
+    g = torch.Generator().manual_seed(seed)
+    det = torch.zeros(B, 5, N)
+    gts, gidx = [], []
+    for i in range(B):
+        ng = [3, 0, 2, 4, 1, 2][i]
+        c = torch.rand(ng, 2, generator=g) * 400
+        gb = torch.cat([c, c + torch.rand(ng, 2, generator=g) * 80 + 20], 1)
+        gts.append(gb)
+        gidx += [i] * ng
+        k = torch.randint(0, max(ng, 1), (N,), generator=g)
+        base = gb[k] if ng else torch.rand(N, 4, generator=g) * 400
+        pb = base + (torch.rand(N, 4, generator=g) - 0.5) * 30
+        sc = torch.rand(N, generator=g)
+        if i == 2:
+            sc = sc * 0.009                       # nothing above the 0.01 filter
+        if i == 3:
+            pb = pb + 1000                        # kept, but no positive
+        if i == 5:
+            # eight kept positives and a single kept negative (a one-element background mean)
+            sc = torch.where(torch.arange(N) < 9, sc * 0.5 + 0.5, sc * 0.005)
+            pb[:8] = gb[k[:8]] + (torch.rand(8, 4, generator=g) - 0.5) * 2
+            pb[8] = pb[8] + 1000
+        det[i, :4] = pb.t()
+        det[i, 4] = sc
+    return det, torch.cat(gts, 0), torch.tensor(gidx, dtype=torch.int64)
+
+
+def golden_loss(module_cls):
+    class _M(torch.nn.Module):
+        def set_task(self, t):
+            pass
+    mod = module_cls(_M())
+    det, gt, gidx = loss_inputs()
+    boxes, scores = mod.process_yolo_output(det, is_training=False)
+    import contextlib, io
+    with contextlib.redirect_stdout(io.StringIO()):
+        loss, d = mod.compute_loss(boxes, scores, {"boxes": gt, "labels": torch.zeros(len(gt), dtype=torch.int64),
+                                                   "batch_idx": gidx})
+    per = np.full((det.shape[0], 4), np.nan)
+    for b in range(det.shape[0]):
+        if f"box_loss_{b}" in d:
+            per[b] = [d[f"box_loss_{b}"] + d[f"cls_loss_{b}"] + 0.5 * d[f"bg_loss_{b}"], d[f"box_loss_{b}"],
+                      d[f"cls_loss_{b}"], d[f"bg_loss_{b}"]]
+        elif f"bg_loss_{b}" in d:
+            per[b] = [d[f"bg_loss_{b}"], np.nan, np.nan, d[f"bg_loss_{b}"]]
+    path = os.path.join(ROOT, "tests", "golden", "golden_detloss.npz")
+    np.savez_compressed(path, det=det.numpy(), gt=gt.numpy(), gtidx=gidx.numpy(), loss=np.float64(loss.item()),
+                        per_image=per)
+    print(path, loss.item())
+
+
 def main():
     ref_shims.install()
-    from lightning.face_detection.module_v2 import DetectionMetrics  # the reference class
+    from lightning.face_detection.module_v2 import DetectionMetrics, FaceDetectionModule  # the reference
+    golden_loss(FaceDetectionModule)
 
     m = DetectionMetrics()
     out = {}

@@ -471,3 +471,70 @@ class DetectionMetricsRef:
             aps.append(torch.trapz(prec, rec).item())
         return {"precision": precision, "recall": recall, "f1": f1, "mAP50": aps[0], "mAP75": aps[5],
                 "mAP": sum(aps) / len(aps)}
+
+
+def compute_iou_ref(box1: Tensor, box2: Tensor, eps=1e-7, CIoU=False) -> Tensor:
+    """training/lightning/utils.py:8-76 restated (pairwise [N, M])."""
+    b1 = box1.unsqueeze(1)
+    b2 = box2.unsqueeze(0)
+    b1x1, b1y1, b1x2, b1y2 = b1.split(1, dim=-1)
+    b2x1, b2y1, b2x2, b2y2 = b2.split(1, dim=-1)
+    w1, h1, w2, h2 = b1x2 - b1x1, b1y2 - b1y1, b2x2 - b2x1, b2y2 - b2y1
+    area1 = w1.clamp(min=0) * h1.clamp(min=0)
+    area2 = w2.clamp(min=0) * h2.clamp(min=0)
+    iw = (torch.minimum(b1x2, b2x2) - torch.maximum(b1x1, b2x1)).clamp(min=0)
+    ih = (torch.minimum(b1y2, b2y2) - torch.maximum(b1y1, b2y1)).clamp(min=0)
+    inter = iw * ih
+    iou = inter / (area1 + area2 - inter + eps)
+    if not CIoU:
+        return iou.squeeze(-1)
+    cw = torch.maximum(b1x2, b2x2) - torch.minimum(b1x1, b2x1)
+    ch = torch.maximum(b1y2, b2y2) - torch.minimum(b1y1, b2y1)
+    c2 = (cw ** 2 + ch ** 2) + eps
+    rho2 = ((b1x1 + b1x2 - b2x1 - b2x2) ** 2 + (b1y1 + b1y2 - b2y1 - b2y2) ** 2) / 4
+    v = (4 / (math.pi ** 2)) * torch.pow(torch.atan(w2 / (h2 + eps)) - torch.atan(w1 / (h1 + eps)), 2)
+    alpha = v / (v - iou + (1 + eps))
+    return (iou - (rho2 / c2 + v * alpha)).squeeze(-1)
+
+
+def detection_eval_loss_ref(pred_boxes: Tensor, pred_scores: Tensor, gt_boxes: Tensor, gt_labels: Tensor,
+                            batch_idx: Tensor):
+    """FaceDetectionModule.compute_loss (module_v2.py:178-303) restated: returns (avg_loss,
+    {image: (loss_b, box, cls, bg)}) with NaN for terms the reference does not compute."""
+    B = pred_boxes.shape[0]
+    if pred_boxes.shape[1] == 4:
+        pred_boxes = pred_boxes.transpose(1, 2)
+        pred_scores = pred_scores.transpose(1, 2)
+    max_scores, _ = pred_scores.max(dim=-1)
+    total = 0
+    per = {}
+    nan = float("nan")
+    for b in range(B):
+        mask = batch_idx == b
+        if not mask.any():
+            continue
+        g, gl = gt_boxes[mask], gt_labels[mask]
+        conf = max_scores[b] > 0.01
+        pb, ps = pred_boxes[b, conf], pred_scores[b, conf]
+        if len(pb) == 0 or len(g) == 0:
+            if len(pb) > 0:
+                bg = F.binary_cross_entropy_with_logits(ps.max(dim=-1)[0], torch.zeros_like(ps.max(dim=-1)[0]))
+                total += bg
+                per[b] = (bg.item(), nan, nan, bg.item())
+            continue
+        ious = compute_iou_ref(pb, g)
+        best, idx = ious.max(dim=1)
+        pos = best > 0.5
+        if pos.any():
+            box = -compute_iou_ref(pb[pos], g[idx[pos]], CIoU=True).mean()
+            cls = F.cross_entropy(ps[pos], gl[idx[pos]])
+            bgv = ps[~pos].max(dim=-1)[0]
+            bg = F.binary_cross_entropy_with_logits(bgv, torch.zeros_like(bgv))
+            lb = box + cls + 0.5 * bg
+            total += lb
+            per[b] = (lb.item(), box.item(), cls.item(), bg.item())
+        else:
+            bg = F.binary_cross_entropy_with_logits(ps.max(dim=-1)[0], torch.zeros_like(ps.max(dim=-1)[0]))
+            total += bg
+            per[b] = (bg.item(), nan, nan, bg.item())
+    return total / B, per

@@ -331,3 +331,195 @@ extern "C" int prpe_det_metrics_compute(const uint64_t* counters, const float* r
                      (const int*)totals, (const double*)tile_area, tiles, out);
   return launch_status();
 }
+
+// ------------------------------------------------------------------ detection eval loss
+// FaceDetectionModule.compute_loss (module_v2.py:178-303) on the eval-mode head output, as
+// validation_step calls it (:467): boxes [B, 4, N] (taken as x1y1x2y2 by compute_iou, as the
+// reference does), scores [B, C, N]; one block per image:
+//   keep = max_c score > 0.01 (order kept); no ground truth in the image: skipped (loss 0);
+//   no kept prediction or no box: bg loss on the kept ones if any;
+//   else ious = compute_iou(kept, gt) (utils.py:8-76, eps 1e-7), best = max over gt (first
+//   index on ties), pos = best > 0.5; with positives: box = -mean over the P x P matrix
+//   compute_iou(kept[pos], gt[idx[pos]], CIoU=True) (the reference takes the mean of the full
+//   pairwise matrix), cls = cross_entropy(scores[pos], gt_class[idx[pos]]), bg = mean BCE-
+//   with-logits(max score of the non-positives, 0); loss_b = box + cls + 0.5 bg;
+//   without positives: loss_b = bg over all kept. loss = sum_b loss_b / B.
+namespace {
+
+constexpr int LOSS_MAX_N = 1024;
+
+__device__ __forceinline__ float bce0(float x) {
+  // F.binary_cross_entropy_with_logits(x, 0): (1 - 0) x + max_val + log(exp(-max_val) + exp(-x - max_val))
+  const float m = fmaxf(-x, 0.f);
+  return x + m + logf(expf(-m) + expf(-x - m));
+}
+
+// compute_iou (utils.py:8-76) for one pair, fp32 in the reference's operation order
+__device__ float ref_iou(const float* a, const float* b, bool ciou) {
+  const float eps = 1e-7f;
+  const float w1 = a[2] - a[0], h1 = a[3] - a[1], w2 = b[2] - b[0], h2 = b[3] - b[1];
+  const float area1 = fmaxf(w1, 0.f) * fmaxf(h1, 0.f), area2 = fmaxf(w2, 0.f) * fmaxf(h2, 0.f);
+  const float iw = fmaxf(fminf(a[2], b[2]) - fmaxf(a[0], b[0]), 0.f);
+  const float ih = fmaxf(fminf(a[3], b[3]) - fmaxf(a[1], b[1]), 0.f);
+  const float inter = iw * ih;
+  const float uni = area1 + area2 - inter + eps;
+  const float iou = inter / uni;
+  if (!ciou) return iou;
+  const float cw = fmaxf(a[2], b[2]) - fminf(a[0], b[0]);
+  const float ch = fmaxf(a[3], b[3]) - fminf(a[1], b[1]);
+  const float c2 = (cw * cw + ch * ch) + eps;
+  const float dx = a[0] + a[2] - b[0] - b[2], dy = a[1] + a[3] - b[1] - b[3];
+  const float rho2 = (dx * dx + dy * dy) / 4.f;
+  const float d = atanf(w2 / (h2 + eps)) - atanf(w1 / (h1 + eps));
+  const float v = (float)(4.0 / (M_PI * M_PI)) * (d * d);       // Python-float constant, cast to fp32
+  const float alpha = v / (v - iou + (1.f + eps));
+  return iou - (rho2 / c2 + v * alpha);
+}
+
+struct LossK {
+  const float* boxes; int64_t bs_b, bs_c, bs_n;     // [B, 4, N] element strides
+  const float* scores; int64_t ss_b, ss_c, ss_n;    // [B, C, N]
+  int B, C, N;
+  const float* gt; const int64_t* gt_batch; const int64_t* gt_cls; int G;
+  float* per_image;                                 // [B][4]: loss_b, box, cls, bg (NaN = not computed)
+};
+
+__global__ __launch_bounds__(256) void det_loss_kernel(LossK p) {
+  const int b = blockIdx.x;
+  __shared__ int keep_idx[LOSS_MAX_N];
+  __shared__ float best_s[LOSS_MAX_N];
+  __shared__ int gidx_s[LOSS_MAX_N];
+  __shared__ int nkeep, npos, ngt;
+  __shared__ double red[4];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    // kept predictions in order, and the image's ground-truth count
+    int k = 0;
+    for (int j = 0; j < p.N; ++j) {
+      float m = -INFINITY;
+      for (int c = 0; c < p.C; ++c) m = fmaxf(m, p.scores[b * p.ss_b + c * p.ss_c + (int64_t)j * p.ss_n]);
+      if (m > 0.01f) keep_idx[k++] = j;
+    }
+    nkeep = k;
+    int g = 0;
+    for (int q = 0; q < p.G; ++q) g += p.gt_batch[q] == b;
+    ngt = g;
+    npos = 0;
+    for (int q = 0; q < 4; ++q) red[q] = 0.0;
+  }
+  __syncthreads();
+  float* out = p.per_image + (int64_t)b * 4;
+  if (ngt == 0) {                                   // "No targets in this batch, skipping"
+    if (tid == 0) { out[0] = 0.f; out[1] = out[2] = out[3] = NAN; }
+    return;
+  }
+  auto maxscore = [&](int j) {
+    float m = -INFINITY;
+    for (int c = 0; c < p.C; ++c) m = fmaxf(m, p.scores[b * p.ss_b + c * p.ss_c + (int64_t)j * p.ss_n]);
+    return m;
+  };
+  auto box_of = [&](int j, float* o) {
+    for (int c = 0; c < 4; ++c) o[c] = p.boxes[b * p.bs_b + c * p.bs_c + (int64_t)j * p.bs_n];
+  };
+  const int M = nkeep;
+  // best IoU over the image's ground truth per kept prediction (first index on ties)
+  for (int k = tid; k < M; k += blockDim.x) {
+    float a[4];
+    box_of(keep_idx[k], a);
+    float best = 0.f;
+    int bi = -1, gl = 0;
+    for (int q = 0; q < p.G; ++q) {
+      if (p.gt_batch[q] != b) continue;
+      const float v = ref_iou(a, p.gt + (int64_t)q * 4, false);
+      if (bi < 0 || v > best || (v != v && best == best)) { best = v; bi = q; }
+      ++gl;
+    }
+    best_s[k] = best;
+    gidx_s[k] = bi;
+    if (best > 0.5f) atomicAdd(&npos, 1);
+  }
+  __syncthreads();
+  const int P = npos;
+  // positives in order (prefix by one thread: M <= LOSS_MAX_N)
+  __shared__ int pos_idx[LOSS_MAX_N];
+  __shared__ int neg_cnt;
+  if (tid == 0) {
+    int q = 0, r = 0;
+    for (int k = 0; k < M; ++k) {
+      if (best_s[k] > 0.5f) pos_idx[q++] = k;
+      else ++r;
+    }
+    neg_cnt = r;
+  }
+  __syncthreads();
+  if (M == 0) {
+    if (tid == 0) { out[0] = 0.f; out[1] = out[2] = out[3] = NAN; }
+    return;
+  }
+  double bg = 0.0, box = 0.0, cls = 0.0;
+  if (P == 0) {
+    for (int k = tid; k < M; k += blockDim.x) bg += (double)bce0(maxscore(keep_idx[k]));
+  } else {
+    for (int k = tid; k < M; k += blockDim.x)
+      if (!(best_s[k] > 0.5f)) bg += (double)bce0(maxscore(keep_idx[k]));
+    // box: mean of the P x P CIoU matrix between positives i and matched boxes of positives j
+    for (int e = tid; e < P * P; e += blockDim.x) {
+      const int i = e / P, jj = e % P;
+      float a[4];
+      box_of(keep_idx[pos_idx[i]], a);
+      box += (double)ref_iou(a, p.gt + (int64_t)gidx_s[pos_idx[jj]] * 4, true);
+    }
+    // cross_entropy(scores[pos] [P, C], labels): logsumexp - score[label]
+    for (int i = tid; i < P; i += blockDim.x) {
+      const int j = keep_idx[pos_idx[i]];
+      const int64_t lab = p.gt_cls ? p.gt_cls[gidx_s[pos_idx[i]]] : 0;
+      float m = -INFINITY;
+      for (int c = 0; c < p.C; ++c) m = fmaxf(m, p.scores[b * p.ss_b + c * p.ss_c + (int64_t)j * p.ss_n]);
+      float s = 0.f;
+      for (int c = 0; c < p.C; ++c) s += expf(p.scores[b * p.ss_b + c * p.ss_c + (int64_t)j * p.ss_n] - m);
+      cls += (double)(m + logf(s) - p.scores[b * p.ss_b + lab * p.ss_c + (int64_t)j * p.ss_n]);
+    }
+  }
+  atomicAdd(&red[0], bg);
+  atomicAdd(&red[1], box);
+  atomicAdd(&red[2], cls);
+  __syncthreads();
+  if (tid == 0) {
+    if (P == 0) {
+      const float bgm = (float)(red[0] / M);
+      out[0] = bgm; out[1] = NAN; out[2] = NAN; out[3] = bgm;
+    } else {
+      const float boxm = -(float)(red[1] / ((double)P * P));
+      const float clsm = (float)(red[2] / P);
+      const float bgm = neg_cnt > 0 ? (float)(red[0] / neg_cnt) : NAN;   // mean of an empty tensor
+      out[0] = boxm + clsm + 0.5f * bgm; out[1] = boxm; out[2] = clsm; out[3] = bgm;
+    }
+  }
+}
+
+__global__ void det_loss_mean_kernel(const float* per_image, int B, float* loss) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float t = 0.f;
+  for (int b = 0; b < B; ++b) t += per_image[b * 4];
+  loss[0] = t / (float)B;
+}
+
+}  // namespace
+
+extern "C" int prpe_det_eval_loss(const float* boxes, const int64_t* box_strides, const float* scores,
+                                  const int64_t* score_strides, int32_t B, int32_t C, int32_t N,
+                                  const float* gt_boxes, const int64_t* gt_batch, const int64_t* gt_classes,
+                                  int32_t G, float* per_image, float* loss, void* stream) {
+  if (!boxes || !box_strides || !scores || !score_strides || B <= 0 || C <= 0 || N <= 0 || N > LOSS_MAX_N ||
+      G < 0 || (G > 0 && (!gt_boxes || !gt_batch)) || !per_image || !loss)
+    return PRPE_EINVAL;
+  LossK p{};
+  p.boxes = boxes; p.bs_b = box_strides[0]; p.bs_c = box_strides[1]; p.bs_n = box_strides[2];
+  p.scores = scores; p.ss_b = score_strides[0]; p.ss_c = score_strides[1]; p.ss_n = score_strides[2];
+  p.B = B; p.C = C; p.N = N; p.gt = gt_boxes; p.gt_batch = gt_batch; p.gt_cls = gt_classes; p.G = G;
+  p.per_image = per_image;
+  hipStream_t st = as_stream(stream);
+  hipLaunchKernelGGL(det_loss_kernel, dim3(B), dim3(256), 0, st, p);
+  hipLaunchKernelGGL(det_loss_mean_kernel, dim3(1), dim3(64), 0, st, (const float*)per_image, B, loss);
+  return launch_status();
+}

@@ -70,6 +70,7 @@ SIGNATURES = {
     "prpe_det_metrics_update": (C.c_int, [_P, _P, _I, _I, _P, _P, _I, _P, _P, _L, _P, _L, _P]),
     "prpe_det_metrics_compute_workspace_bytes": (C.c_int64, [_L]),
     "prpe_det_metrics_compute": (C.c_int, [_P, _P, _L, _P, _P, _P, _L, _P]),
+    "prpe_det_eval_loss": (C.c_int, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P]),
     "prpe_abi_version": (C.c_int, []),
     "prpe_build_info": (C.c_char_p, []),
 }

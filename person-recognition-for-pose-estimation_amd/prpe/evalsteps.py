@@ -17,6 +17,9 @@
   per batch one launch matches the padded NMS output against the ground truth and appends
   (score, best IoU) records on device (prpe_det_metrics_update); compute() at epoch end
   (prpe_det_metrics_compute) returns the reference's dict.
+* ``detection_eval_loss`` — the same step's compute_loss (module_v2.py:178-303) on the eval
+  head output: one block per image (confidence filter, IoU matching, the pairwise CIoU mean,
+  cross-entropy, background BCE), no per-image host sync (prpe_det_eval_loss).
 """
 from __future__ import annotations
 
@@ -115,3 +118,11 @@ class DetectionMetricsDevice:
             raise RuntimeError(f"DetectionMetricsDevice: {n} records exceed the capacity {self.records.shape[0]}")
         out = ops.det_metrics_compute(self.counters, self.records, n, self.THRESHOLDS).tolist()
         return dict(zip(self.KEYS, out))
+
+
+@torch.no_grad()
+def detection_eval_loss(det, gt_boxes, gt_batch, gt_labels=None):
+    """(avg_loss [1], per_image [B, 4] = (loss_b, box, cls, bg)) for the eval-mode detection
+    output ``det`` [B, 4+nc, N] (FaceDetectionModule.process_yolo_output's eval split:
+    boxes det[:, :4], scores det[:, 4:]) against targets boxes / batch_idx / labels."""
+    return ops.det_eval_loss(det[:, :4], det[:, 4:], gt_boxes, gt_batch, gt_labels)

@@ -225,3 +225,23 @@ def det_metrics_compute(counters, records, n, thresholds):
     check(lib().prpe_det_metrics_compute(counters.data_ptr(), records.data_ptr(), n, C.cast(thr, C.c_void_p),
                                          out.data_ptr(), ws.data_ptr(), nbytes, _stream()), "prpe_det_metrics_compute")
     return out
+
+
+def det_eval_loss(boxes, scores, gt_boxes, gt_batch, gt_classes=None):
+    """Detection eval loss (see include/prpe.h): boxes [B,4,N], scores [B,C,N] (any strides).
+    Returns (loss [1], per_image [B,4] = (loss_b, box, cls, bg))."""
+    B, four, N = boxes.shape
+    Cn = scores.shape[1]
+    assert four == 4 and scores.shape[0] == B and scores.shape[2] == N
+    dev = boxes.device
+    gt = gt_boxes.to(device=dev, dtype=torch.float32).contiguous().view(-1, 4)
+    gb = gt_batch.to(device=dev, dtype=torch.int64).contiguous().view(-1)
+    gc = None if gt_classes is None else gt_classes.to(device=dev, dtype=torch.int64).contiguous().view(-1)
+    bs = (C.c_int64 * 3)(*boxes.stride())
+    ss = (C.c_int64 * 3)(*scores.stride())
+    per = torch.empty(B, 4, device=dev, dtype=torch.float32)
+    loss = torch.empty(1, device=dev, dtype=torch.float32)
+    check(lib().prpe_det_eval_loss(boxes.data_ptr(), C.cast(bs, C.c_void_p), scores.data_ptr(), C.cast(ss, C.c_void_p),
+                                   B, Cn, N, gt.data_ptr(), gb.data_ptr(), _ptr(gc), gt.shape[0], per.data_ptr(),
+                                   loss.data_ptr(), _stream()), "prpe_det_eval_loss")
+    return loss, per

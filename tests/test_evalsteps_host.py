@@ -57,3 +57,24 @@ def test_detection_metrics_oracle_matches_reference_golden():
     assert any(r[2] == 0.5 for r in m.records)                       # IoU exactly 0.5: not a TP
     scores = [r[0] for r in m.records]
     assert len(set(scores)) < len(scores)                            # tied scores
+
+
+def test_detection_eval_loss_oracle_matches_reference_golden():
+    """oracle.detection_eval_loss_ref == the reference's FaceDetectionModule.compute_loss on
+    its own fixtures (oracle/make_golden_detmetrics.py): the batch loss and each image's
+    terms, incl. images without ground truth, without kept predictions, without positives."""
+    import math
+    import os
+    import numpy as np
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_detloss.npz")))
+    det = torch.from_numpy(g["det"])
+    gt, gidx = torch.from_numpy(g["gt"]), torch.from_numpy(g["gtidx"])
+    loss, per = R.detection_eval_loss_ref(det[:, :4], det[:, 4:5], gt, torch.zeros(len(gt), dtype=torch.int64), gidx)
+    assert abs(loss.item() - float(g["loss"])) <= 1e-6
+    for b in range(det.shape[0]):
+        exp = g["per_image"][b]
+        if math.isnan(exp[0]):
+            assert b not in per
+            continue
+        for v, e in zip(per[b], exp):
+            assert (math.isnan(v) and math.isnan(e)) or abs(v - e) <= 1e-6, (b, per[b], exp)

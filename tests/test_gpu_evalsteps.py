@@ -159,3 +159,39 @@ def test_detection_metrics_device_large_vs_oracle():
     out, exp = m.compute(), ref.compute()
     for k in exp:
         assert abs(out[k] - exp[k]) <= 1e-5 * max(1.0, abs(exp[k])), (k, out[k], exp[k])
+
+
+def test_detection_eval_loss_device_vs_reference_golden():
+    """Device compute_loss on the reference's own fixtures: batch loss and per-image terms
+    (fp32 libm and reduction order: 2e-5)."""
+    import math
+    import os
+    import numpy as np
+    from prpe.evalsteps import detection_eval_loss
+    g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", "golden_detloss.npz")))
+    det = torch.from_numpy(g["det"]).cuda()
+    loss, per = detection_eval_loss(det, torch.from_numpy(g["gt"]).cuda(), torch.from_numpy(g["gtidx"]).cuda())
+    torch.cuda.synchronize()
+    assert abs(loss.item() - float(g["loss"])) <= 2e-5
+    per = per.cpu().double().numpy()
+    for b in range(det.shape[0]):
+        exp = g["per_image"][b]
+        if math.isnan(exp[0]):
+            assert per[b, 0] == 0.0          # no term for this image
+            continue
+        for v, e in zip(per[b], exp):
+            assert (math.isnan(v) and math.isnan(e)) or abs(v - e) <= 2e-5, (b, per[b], exp)
+
+
+def test_detection_eval_loss_all_positive_is_nan_like_the_reference():
+    """Every kept prediction positive: the reference's background mean is over an empty tensor
+    (NaN), so its loss is NaN; the device kernel reproduces it."""
+    from prpe.evalsteps import detection_eval_loss
+    gt = torch.tensor([[10., 10., 50., 60.]])
+    det = torch.zeros(1, 5, 4)
+    det[0, :4] = torch.tensor([[10., 10., 50., 60.]] * 2 + [[0., 0., 1., 1.]] * 2).t()
+    det[0, 4] = torch.tensor([0.9, 0.8, 0.001, 0.002])
+    loss, per = detection_eval_loss(det.cuda(), gt.cuda(), torch.zeros(1, dtype=torch.int64).cuda())
+    ref_loss, _ = R.detection_eval_loss_ref(det[:, :4], det[:, 4:5], gt, torch.zeros(1, dtype=torch.int64),
+                                            torch.zeros(1, dtype=torch.int64))
+    assert torch.isnan(ref_loss) and torch.isnan(loss.cpu()).all()
