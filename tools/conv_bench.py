@@ -47,6 +47,8 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--korders", default="0,1", help="weight K orders to compare (1 = chunk-major)")
     ap.add_argument("--amax", action="store_true", help="also track max|y| (y_amax) in the epilogue")
+    ap.add_argument("--planes", action="store_true",
+                    help="input in the planes format (x_planes; precision 0, wave-row kernel)")
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -72,7 +74,7 @@ def main():
           for prec in [int(v) for v in a.prec.split(",")]:
             for tile in [int(v) for v in a.tiles.split(",")]:
                 kw = dict(res=r, res_mode=1 if r is not None else 0, precision=prec, tile=tile, y_amax=ya,
-                          x_amax=xa if prec == 3 else None)
+                          x_amax=xa if prec == 3 else None, x_planes=a.planes)
                 try:
                     ops.conv2d(x, pk, y, **kw)
                 except Exception as ex:              # tile not eligible for this shape
