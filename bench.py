@@ -144,7 +144,8 @@ def main():
         fl = conv_flops(p, pixels)
         passes = {0: 3, 1: 1, 2: 6}[precn]
         ach = fl / avg_s / 1e12
-        roof = {"bound": "mfma", "kernel": f"conv_igemm[{args.dominant}] {p.kh}x{p.kw} {p.ci}->{p.co}",
+        roof = {"bound": "mfma", "kernel": f"prpe_conv2d[{args.dominant}] {p.kh}x{p.kw} {p.ci}->{p.co} "
+                                           f"(conv_wave_kernel, auto tile)",
                 "achieved": round(ach, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
                 "executed_mfma_passes": passes,
