@@ -41,6 +41,10 @@ AUTO_POLICY = {"trunk": 3, "yolo_adapter": 0, "yolo_net": 2, "adaface": 0, "vit"
 AMAX_SLOTS = 4096
 # PRPE_PLANES=0 keeps every activation in fp32 (A/B runs of the planes-format handoff)
 PLANES_ON = os.environ.get("PRPE_PLANES", "1") != "0"
+# 3x3/1 convs with Co <= 4 (the last conv of the YOLO and ViTPose adapters) as the tap rewrite
+# at unit scale: one read of the input by a 1x1 GEMM to the 9*Co tap maps, then a shifted tap
+# sum (prpe_upconv3x3 with an identity resample). PRPE_SMALLCO_TAPS=0 keeps the direct conv.
+SMALLCO_TAPS = os.environ.get("PRPE_SMALLCO_TAPS", "1") != "0"
 
 
 class _Prec:
@@ -212,6 +216,17 @@ class Engine:
             out._prpe_planes = True
         return out
 
+    def conv3x3_smallco(self, x, name, wkey, bn=None, bias_key=None, act="none"):
+        """3x3 stride-1 pad-1 conv + BN + act for Co <= 4. The direct implicit GEMM re-reads
+        the input once per tap for 3 useful output columns; here z = x W_taps (1x1, 9*Co
+        outputs, the input read once) and y = act(BN(sum_tap shift_tap(z_tap))) by the tap
+        sum of ``upconv`` with the output grid equal to the input grid (align_corners=True at
+        unit scale: every source index is exact, interpolation weights 1 and 0). Same
+        function as the conv; fp32 summation order differs."""
+        if SMALLCO_TAPS:
+            return self.upconv(name, x, wkey, (x.shape[1], x.shape[2]), True, bn=bn, bias_key=bias_key, act=act)
+        return self.conv(x, self.pk(name, wkey, 1, 1, bn=bn, bias_key=bias_key, act=act))
+
     # ------------------------------------------------------------------ ResNet-50 trunk
     def trunk(self, x_nchw, flip_w=False):
         """MultiTaskResNetFeatureExtractor (modify_models.py:427-437), torchvision v1.5.
@@ -363,8 +378,8 @@ class Engine:
         t = self.conv(t, self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias",
                                  act="silu"))
         t = self.conv(t, self.pk(a + ".13", a + ".13.weight", bn=a + ".14", bias_key=a + ".13.bias", act="silu"))
-        t = self.conv(t, self.pk(a + ".16", a + ".16.weight", 1, 1, bn=a + ".17", bias_key=a + ".16.bias",
-                                 act="silu"))
+        t = self.conv3x3_smallco(t, a + ".16", a + ".16.weight", bn=a + ".17", bias_key=a + ".16.bias",
+                                 act="silu")
         return ops.norm_sigmoid(t, self.empty(*t.shape))
 
     def yolo_net(self, p, s, stride):
@@ -475,8 +490,8 @@ class Engine:
         u = self.upconv(a + ".4", t, a + ".4.weight", arch.VIT_IMG, True, bn=a + ".5", bias_key=a + ".4.bias",
                         act="gelu", planes=True)
         t = self.conv(u, self.pk(a + ".7", a + ".7.weight", 1, 1, bn=a + ".8", bias_key=a + ".7.bias", act="gelu"))
-        return self.conv(t, self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias",
-                                    act="gelu"))
+        return self.conv3x3_smallco(t, a + ".10", a + ".10.weight", bn=a + ".11", bias_key=a + ".10.bias",
+                                    act="gelu")
 
     def _lin(self, name, wkey, bkey, act="none"):
         p = self._packs.get(name)

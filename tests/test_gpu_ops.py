@@ -534,6 +534,29 @@ def test_upconv_equals_upsample_then_conv(hi, wi, ho, wo, ac, act, separable):
     torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=2e-4)
 
 
+@pytest.mark.parametrize("h,w,ci,co,act", [(256, 192, 128, 3, "gelu"), (160, 160, 64, 3, "silu"),
+                                         (7, 5, 32, 1, "none"), (1, 1, 64, 4, "silu"), (13, 29, 96, 2, "gelu")])
+def test_conv3x3_smallco_tap_rewrite(h, w, ci, co, act):
+    """Engine.conv3x3_smallco: a 3x3/1 pad-1 conv with Co <= 4 as the 1x1 tap GEMM plus the
+    unit-scale tap sum of prpe_upconv3x3 (align_corners=True, output grid = input grid, so
+    every source index is exact). Against the direct conv in fp64; tolerance as the other
+    split-bf16 convs (2e-4 abs on O(1) data, K = 9*ci)."""
+    x = rnd(2, ci, h, w, seed=230)
+    wt = rnd(co, ci, 3, 3, seed=231, scale=0.05)
+    sc = torch.rand(co, generator=_g(232)) + 0.5
+    bi = rnd(co, seed=233)
+    taps = pack.pack_upconv_taps("t", wt, DEV)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    z = torch.empty(2, h, w, 9 * co, device=DEV)
+    ops.conv2d(xd, taps, z)
+    y = torch.empty(2, h, w, co, device=DEV)
+    ops.upconv3x3(z, y, True, sc.to(DEV), bi.to(DEV), None, act)
+    torch.cuda.synchronize()
+    ref = F.conv2d(x.double(), wt.double(), None, 1, 1) * sc.double().view(1, -1, 1, 1) + bi.double().view(1, -1, 1, 1)
+    ref = act_ref(ref.float(), act)
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=2e-4)
+
+
 @pytest.mark.parametrize("hi,wi,ho,wo,ac", [(20, 20, 160, 160, True), (20, 20, 256, 192, True),
                                         (16, 12, 64, 48, False), (7, 9, 20, 13, False), (20, 20, 23, 21, True)])
 def test_upconv_fused_matches_separable(hi, wi, ho, wo, ac):
