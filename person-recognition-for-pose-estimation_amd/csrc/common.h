@@ -18,15 +18,30 @@ static inline int launch_status() {
   return e == hipSuccess ? 0 : static_cast<int>(e);
 }
 
-// Activation applied in every epilogue. Accurate libm forms (expf/erff), not fast-math,
-// so results track the fp32 CPU reference to a few ulp.
+// exp(x) from the hardware base-2 exponential (v_exp_f32, 1 ulp) with x*log2(e) carried in
+// two parts (t + e), so the argument rounding does not grow with |x|: 2^(t+e) = 2^t (1 + e ln2)
+// to ~2 ulp over the normal range; overflows to +inf and underflows to 0 like expf.
+// 1 + e ln2 is within 2^-20 of 1, so it is finite and positive.
+__device__ __forceinline__ float exp_hw(float x) {
+  const float L = 1.44269502162933349609375f;     // log2(e) rounded to fp32
+  const float Llo = 1.925963033500011e-08f;       // log2(e) - L
+  const float t = x * L;
+  const float e = fmaf(x, L, -t) + x * Llo;
+  // r * (1 + e ln2), not fma(r, e ln2, r): an overflowed r = inf times a correction below 0
+  // would give inf - inf = NaN
+  return __builtin_amdgcn_exp2f(t) * (1.f + e * 0.693147180559945309f);
+}
+
+// Activation applied in every epilogue, accurate to a few ulp of the fp32 CPU reference:
+// SiLU / sigmoid as v * rcp(1 + exp(-v)) (exp_hw, v_rcp_f32 1 ulp; ~10 VALU instead of the
+// ~25 of expf + an IEEE division), GELU with libm erff.
 __device__ __forceinline__ float apply_act(float v, int act, float slope) {
   switch (act) {
     case PRPE_ACT_RELU: return v > 0.f ? v : 0.f;
-    case PRPE_ACT_SILU: return v / (1.f + expf(-v));
+    case PRPE_ACT_SILU: return v * __builtin_amdgcn_rcpf(1.f + exp_hw(-v));
     case PRPE_ACT_PRELU: return v >= 0.f ? v : v * slope;
     case PRPE_ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752440f));
-    case PRPE_ACT_SIGMOID: return 1.f / (1.f + expf(-v));
+    case PRPE_ACT_SIGMOID: return __builtin_amdgcn_rcpf(1.f + exp_hw(-v));
     default: return v;
   }
 }

@@ -62,21 +62,27 @@ struct UpK {
 // row advances the interval by at most one source row when upsampling, so each H row is built
 // once per thread (6 L2 loads) instead of once per output row. HBM traffic is the output
 // write plus the small z read. Same arithmetic, same order as the separable form.
+// Addressing: the frame / source-row / tap-row part of every address is block-uniform
+// (scalar base), the per-thread part is a loop-invariant 32-bit element offset (the host
+// checks that one frame of z and of y spans < 2^31 elements), so the row loop holds one
+// VGPR per load address and the x-interpolation positions are computed once per thread.
+constexpr int UP_MAX_R = 256;   // longest row range of one fused-kernel block
+struct UpX {        // per-thread x-interpolation of one dx: offsets of columns x0, x1
+  int o0, o1;       // element offsets (x * sw + (dx * Co + c0) * sc) inside a z row
+  float l1;         // weight of x1
+};
+
 template <int VW>
-__device__ __forceinline__ void up_hrow(const UpK& p, int n, int r, int dy, int ox, int c0,
-                                       float (&h)[VW]) {
-  const int Wo = p.y.w, Wi = p.z.w;
+__device__ __forceinline__ void up_hrow(const float* __restrict__ zrow, const UpX (&ux)[3], unsigned xvalid,
+                                       float (&h)[VW], int sc) {
 #pragma unroll
   for (int v = 0; v < VW; ++v) h[v] = 0.f;
 #pragma unroll
   for (int dx = 0; dx < 3; ++dx) {
-    const int xx = ox + dx - 1;
-    if ((unsigned)xx >= (unsigned)Wo) continue;
-    int x0, x1; float lx;
-    bilin_src(xx, Wi, Wo, p.ac, x0, x1, lx);
-    const float* z = p.z.ptr + (int64_t)n * p.z.sn + (int64_t)r * p.z.sh + (int64_t)((dy * 3 + dx) * p.Co + c0) * p.z.sc;
-    const float* a = z + (int64_t)x0 * p.z.sw;
-    const float* b = z + (int64_t)x1 * p.z.sw;
+    if (!((xvalid >> dx) & 1u)) continue;
+    const float lx = ux[dx].l1;
+    const float* a = zrow + ux[dx].o0;
+    const float* b = zrow + ux[dx].o1;
     if constexpr (VW == 4) {
       const float4 A = *reinterpret_cast<const float4*>(a), B = *reinterpret_cast<const float4*>(b);
       h[0] += (1.f - lx) * A.x + lx * B.x;
@@ -89,18 +95,48 @@ __device__ __forceinline__ void up_hrow(const UpK& p, int n, int r, int dy, int 
   }
 }
 
-template <int VW>
+// ACT >= 0: the epilogue activation as a compile-time constant (one activation's code and
+// registers per instantiation); -1 reads p.act
+template <int VW, int ACT>
 __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rblocks) {
   const int chunk = blockIdx.x % p.chunks;
   const int rb_n = blockIdx.x / p.chunks;
   const int n = rb_n / rblocks, oy0 = (rb_n - n * rblocks) * R;
   const int j = chunk * 256 + threadIdx.x;
+  const int Ho = p.y.h, Hi = p.z.h, Wo = p.y.w, Wi = p.z.w;
+  const int oy1 = oy0 + R < Ho ? oy0 + R : Ho;
+  // vertical source rows / weights of the block's output rows (+1 halo row each side), once
+  // per block into LDS: the row loop reads them as wave-uniform scalars (readfirstlane)
+  __shared__ int ty0[UP_MAX_R + 2];
+  __shared__ float tly[UP_MAX_R + 2];
+  for (int t = threadIdx.x; t < oy1 - oy0 + 2; t += 256) {
+    const int yy = oy0 - 1 + t;
+    int y0 = -1, y1; float ly = 0.f;
+    if ((unsigned)yy < (unsigned)Ho) bilin_src(yy, Hi, Ho, p.ac, y0, y1, ly);
+    ty0[t] = y0;
+    tly[t] = ly;
+  }
+  __syncthreads();
   if (j >= p.per_row) return;
   const int cgroups = p.Co / VW;
   const int ox = j / cgroups, c0 = (j - ox * cgroups) * VW;
-  const int Ho = p.y.h, Hi = p.z.h;
-  const int oy1 = oy0 + R < Ho ? oy0 + R : Ho;
+  const int zsw = (int)p.z.sw, zsc = (int)p.z.sc;
 
+  UpX ux[3];
+  unsigned xvalid = 0;
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int xx = ox + dx - 1;
+    int x0 = 0, x1 = 0; float lx = 0.f;
+    if ((unsigned)xx < (unsigned)Wo) {
+      bilin_src(xx, Wi, Wo, p.ac, x0, x1, lx);
+      xvalid |= 1u << dx;
+    }
+    const int co = (dx * p.Co + c0) * zsc;
+    ux[dx].o0 = x0 * zsw + co;
+    ux[dx].o1 = x1 * zsw + co;
+    ux[dx].l1 = lx;
+  }
   float sc[VW], bi[VW], sl[VW];
 #pragma unroll
   for (int v = 0; v < VW; ++v) {
@@ -108,27 +144,33 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
     bi[v] = p.bias ? p.bias[c0 + v] : 0.f;
     sl[v] = p.slope ? p.slope[c0 + v] : 0.f;
   }
+  const float* zn = p.z.ptr + (int64_t)n * p.z.sn;                       // block-uniform
+  const int64_t tap_row = (int64_t)3 * p.Co * p.z.sc;                    // dy step in channels
+  float* yn = p.y.ptr + (int64_t)n * p.y.sn;                             // block-uniform
+  const int yo = ox * (int)p.y.sw + c0 * (int)p.y.sc;                    // per thread
   float hA[3][VW], hB[3][VW];
   int cur[3] = {-2, -2, -2};
-  float* yp = p.y.ptr + (int64_t)n * p.y.sn + (int64_t)ox * p.y.sw + (int64_t)c0 * p.y.sc;
   for (int oy = oy0; oy < oy1; ++oy) {
     float acc[VW];
 #pragma unroll
     for (int v = 0; v < VW; ++v) acc[v] = 0.f;
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
-      const int yy = oy + dy - 1;
-      if ((unsigned)yy >= (unsigned)Ho) continue;
-      int y0, y1; float ly;
-      bilin_src(yy, Hi, Ho, p.ac, y0, y1, ly);
+      // row yy = oy + dy - 1 is table entry oy - oy0 + dy (y0 = -1: outside the image)
+      const int y0 = __builtin_amdgcn_readfirstlane(ty0[oy - oy0 + dy]);
+      if (y0 < 0) continue;
+      const float ly = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                                     __builtin_bit_cast(int, tly[oy - oy0 + dy])));
+      const int y1 = y0 < Hi - 1 ? y0 + 1 : y0;
       if (y0 != cur[dy]) {
+        const float* zt = zn + dy * tap_row;
         if (y0 == cur[dy] + 1) {
 #pragma unroll
           for (int v = 0; v < VW; ++v) hA[dy][v] = hB[dy][v];
         } else {
-          up_hrow<VW>(p, n, y0, dy, ox, c0, hA[dy]);
+          up_hrow<VW>(zt + (int64_t)y0 * p.z.sh, ux, xvalid, hA[dy], zsc);
         }
-        up_hrow<VW>(p, n, y1, dy, ox, c0, hB[dy]);
+        up_hrow<VW>(zt + (int64_t)y1 * p.z.sh, ux, xvalid, hB[dy], zsc);
         cur[dy] = y0;
       }
 #pragma unroll
@@ -136,8 +178,8 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
     }
     float out[VW];
 #pragma unroll
-    for (int v = 0; v < VW; ++v) out[v] = apply_act(acc[v] * sc[v] + bi[v], p.act, sl[v]);
-    float* y = yp + (int64_t)oy * p.y.sh;
+    for (int v = 0; v < VW; ++v) out[v] = apply_act(acc[v] * sc[v] + bi[v], ACT >= 0 ? ACT : p.act, sl[v]);
+    float* y = yn + (int64_t)oy * p.y.sh + yo;
     if constexpr (VW == 4) {
       if (p.y_planes) {
         // channel group c0 / 8 of the pixel: hi[8] then lo[8] (bf16 RNE two-plane split)
@@ -582,13 +624,25 @@ extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t al
     const char* e = getenv("PRPE_UPCONV_R");
     return e ? atoi(e) : 256;
   }();
-  int R = r_env;
+  int R = r_env < UP_MAX_R ? (r_env > 0 ? r_env : 1) : UP_MAX_R;
   while (R > 4 && (int64_t)y->n * ((y->h + R - 1) / R) * p.chunks < 8192) R /= 2;
   const int rblocks = (y->h + R - 1) / R;
   const int64_t nb = (int64_t)y->n * rblocks * p.chunks;
   if (nb >= (1LL << 31)) return PRPE_EINVAL;
-  if (v4) hipLaunchKernelGGL(upconv_fused_kernel<4>, dim3((unsigned)nb), dim3(256), 0, st, p, R, rblocks);
-  else hipLaunchKernelGGL(upconv_fused_kernel<1>, dim3((unsigned)nb), dim3(256), 0, st, p, R, rblocks);
+  // 32-bit per-thread offsets inside one frame (see the fused kernel)
+  auto span = [](const prpe_view* v) {
+    return (int64_t)(v->h - 1) * v->sh + (int64_t)(v->w - 1) * v->sw + (int64_t)(v->c - 1) * v->sc;
+  };
+  if (span(z) >= (1LL << 31) || span(y) >= (1LL << 31) || z->sw < 0 || z->sc < 0 || z->sh < 0 || y->sw < 0 ||
+      y->sc < 0)
+    return PRPE_EINVAL;
+  const dim3 g((unsigned)nb);
+  if (!v4) hipLaunchKernelGGL((upconv_fused_kernel<1, -1>), g, dim3(256), 0, st, p, R, rblocks);
+  else if (act == PRPE_ACT_NONE) hipLaunchKernelGGL((upconv_fused_kernel<4, PRPE_ACT_NONE>), g, dim3(256), 0, st, p, R, rblocks);
+  else if (act == PRPE_ACT_SILU) hipLaunchKernelGGL((upconv_fused_kernel<4, PRPE_ACT_SILU>), g, dim3(256), 0, st, p, R, rblocks);
+  else if (act == PRPE_ACT_PRELU) hipLaunchKernelGGL((upconv_fused_kernel<4, PRPE_ACT_PRELU>), g, dim3(256), 0, st, p, R, rblocks);
+  else if (act == PRPE_ACT_GELU) hipLaunchKernelGGL((upconv_fused_kernel<4, PRPE_ACT_GELU>), g, dim3(256), 0, st, p, R, rblocks);
+  else hipLaunchKernelGGL((upconv_fused_kernel<4, -1>), g, dim3(256), 0, st, p, R, rblocks);
   return launch_status();
 }
 

@@ -557,6 +557,40 @@ def test_conv3x3_smallco_tap_rewrite(h, w, ci, co, act):
     torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=2e-4)
 
 
+@pytest.mark.parametrize("act", ["silu", "sigmoid", "gelu", "relu"])
+def test_epilogue_activation_accuracy(act):
+    """apply_act (every conv / upconv epilogue; SiLU and sigmoid on the hardware exp2 with a
+    two-part argument) against fp64 torch or the fp32 CPU result: within 4 ulp of either plus
+    1e-35 absolute (where exp(-v) overflows fp32 every fp32 form, the CPU one included, gives
+    -0 for values of order -1e-37), and no NaN at overflow (|v| up to 1e4). Driven through
+    prpe_upconv3x3 at unit scale with only the centre tap non-zero, so the epilogue sees v
+    exactly."""
+    v = torch.cat([torch.linspace(-120, 120, 4801), torch.tensor([0.0, -0.0, 1e-30, -1e-30, 88.7, -88.7, 89.5,
+                                                                   -89.5, 104.0, -104.0, 1e4, -1e4, 1e-3, -1e-3])])
+    n = v.numel()
+    W = 64
+    H = (n + W - 1) // W
+    x = torch.zeros(H * W)
+    x[:n] = v
+    z = torch.zeros(1, H, W, 9 * 4)
+    z[0, :, :, 4 * 4] = x.view(H, W)           # tap (dy=1, dx=1), channel 0
+    y = torch.empty(1, H, W, 4, device=DEV)
+    ops.upconv3x3(z.to(DEV), y, True, torch.ones(4, device=DEV), torch.zeros(4, device=DEV), None, act)
+    torch.cuda.synchronize()
+    got = y[0, :, :, 0].reshape(-1)[:n].cpu().double()
+    vd = v.double()
+    ref = {"silu": vd * torch.sigmoid(vd), "sigmoid": torch.sigmoid(vd), "gelu": F.gelu(vd),
+           "relu": F.relu(vd)}[act]
+    # the CPU reference's own fp32 arithmetic (GELU's 1 + erf cancels below v ~ -5 there too)
+    ref32 = {"silu": F.silu(v), "sigmoid": torch.sigmoid(v), "gelu": F.gelu(v), "relu": F.relu(v)}[act].double()
+    assert not torch.isnan(got).any()
+    ulp = torch.finfo(torch.float32).eps * ref.float().double().abs()
+    # GELU: 0.5 v (1 + erf(v / sqrt 2)) inherits erf's absolute rounding (2^-24) times |v|
+    tol = 4 * ulp + 1e-35 + (2.0 ** -22 * vd.abs() if act == "gelu" else 0.0)
+    bad = ((got - ref).abs() > tol) & ((got - ref32).abs() > tol)
+    assert not bad.any(), (v[bad][:8], got[bad][:8], ref[bad][:8])
+
+
 @pytest.mark.parametrize("hi,wi,ho,wo,ac", [(20, 20, 160, 160, True), (20, 20, 256, 192, True),
                                         (16, 12, 64, 48, False), (7, 9, 20, 13, False), (20, 20, 23, 21, True)])
 def test_upconv_fused_matches_separable(hi, wi, ho, wo, ac):
