@@ -44,14 +44,17 @@ __global__ __launch_bounds__(NWAVE * 64) void vit_attention_kernel(const float* 
     const float4 v4 = *reinterpret_cast<const float4*>(base + key * rs + 2 * HD + h * AD + d4);
     const float kv[4] = {k4.x, k4.y, k4.z, k4.w};
     const float vv[4] = {v4.x, v4.y, v4.z, v4.w};
+    bf16x4 khi, klo;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       __bf16 hi, lo;
       split_bf16(kv[j], hi, lo);
-      Kh[key * KROW + d4 + j] = hi; Kl[key * KROW + d4 + j] = lo;
+      khi[j] = hi; klo[j] = lo;
       split_bf16(vv[j], hi, lo);
       Vh[(d4 + j) * VROW + key] = hi; Vl[(d4 + j) * VROW + key] = lo;
     }
+    *reinterpret_cast<bf16x4*>(Kh + key * KROW + d4) = khi;     // one 8-B LDS write per plane
+    *reinterpret_cast<bf16x4*>(Kl + key * KROW + d4) = klo;
   }
 
   // Q fragments straight from global: A[row = query][k = d]
@@ -103,10 +106,10 @@ __global__ __launch_bounds__(NWAVE * 64) void vit_attention_kernel(const float* 
     rmax[r] = m;
     float sum = 0.f;
 #pragma unroll
-    for (int t = 0; t < NWAVE; ++t) { const float e = expf(s[t][r] - m); s[t][r] = e; sum += e; }
+    for (int t = 0; t < NWAVE; ++t) { const float e = exp_hw(s[t][r] - m); s[t][r] = e; sum += e; }
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
-    rsum[r] = sum;
+    rsum[r] = __builtin_amdgcn_rcpf(sum);     // P = e * (1 / sum): one rcp per row
   }
   (void)rmax;
   // O = P V, P chunks of 32 keys (2 tiles) through the per-wave LDS slab
@@ -122,7 +125,7 @@ __global__ __launch_bounds__(NWAVE * 64) void vit_attention_kernel(const float* 
     for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float pv = s[2 * c + tt][r] / rsum[r];
+        const float pv = s[2 * c + tt][r] * rsum[r];
         __bf16 hi, lo;
         split_bf16(pv, hi, lo);
         const int off = (fg * 4 + r) * 40 + tt * 16 + fr;
