@@ -379,8 +379,21 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       const char* e = getenv("PRPE_WAVE_WIDE");
       return e ? atoi(e) : 26;
     }();
+    // PRPE_WAVE_P3_NARROW=<tile> overrides the precision-3 short-K / narrow choice (A/B runs)
+    static const int p3_narrow = [] {
+      const char* e = getenv("PRPE_WAVE_P3_NARROW");
+      return e ? atoi(e) : 25;
+    }();
+    // precision 3 with Co > 64 takes the wide tile at any K: the short-K residual GEMMs of the
+    // trunk (conv3 + residual, K = 64 / 128 / dual 128) run 16-19 % faster on it than on the
+    // 256 x 64 tile at bs = 256 (profiles/r01_conv_bench_sweep_v4.txt; bench +1.2 %);
+    // PRPE_WAVE_P3_SMALLK=0 restores the 256 x 64 tile for K <= 128 (A/B runs)
+    static const int p3_smallk_wide = [] {
+      const char* e = getenv("PRPE_WAVE_P3_SMALLK");
+      return e && e[0] == '0' ? 0 : 1;
+    }();
     if (prec == 0) tile = wide;
-    else if (prec == 3) tile = kp.Co > 64 && kp.K > 128 ? wide : 25;
+    else if (prec == 3) tile = kp.Co > 64 && (kp.K > 128 || p3_smallk_wide) ? wide : p3_narrow;
     else tile = kp.Co > 64 && kp.K > 128 ? 21 : 24;
   }
   if (prec == 0) {
