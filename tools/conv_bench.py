@@ -36,6 +36,7 @@ SHAPES = {
     "vit proj 768->768 (192 tok)": (16, 12, 768, 768, 1, 1, 0),
     "yolo_adapter.16 3x3 64->3 @160": (160, 160, 64, 3, 3, 1, 1),
     "yolo_adapter.13 1x1 128->64 @160": (160, 160, 128, 64, 1, 1, 0),
+    "ir50 output 7x7 512->512 @7 (M = frames)": (7, 7, 512, 512, 7, 1, 0),
     "ada_adapter.10 3x3 128->64 @112": (112, 112, 128, 64, 3, 1, 1),
     "ada body.0 3x3 64->64 @112": (112, 112, 64, 64, 3, 1, 1),
     "trunk l2 conv3 1x1 128->512 +res @80": (80, 80, 128, 512, 1, 1, 0, "res"),
