@@ -370,14 +370,16 @@ bool conv_wave_eligible(const ConvK& kp, int prec, int km) {
 // tile 20 = auto; 21.. force a configuration (tools/conv_bench.py sweeps them)
 int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
   if (tile == 20) {
-    // measured (tools/conv_bench.py, profiles/r01_conv_bench_wave.txt, r01_conv_bench_tiles_v3.txt):
-    // two planes run 32x128 waves in 4-wave 128x128 blocks (3 waves/SIMD: more blocks in
-    // flight, finer tail on the ViT / IR-50 GEMM shapes), short-K or narrow convs the 256x64
-    // tile; three bf16 planes 32-row waves
+    // measured (tools/conv_bench.py, profiles/r01_conv_bench_wave.txt, r01_conv_bench_tiles_v3.txt,
+    // r01_conv_bench_stages.txt): 32x128 waves in 4-wave 128x128 blocks with a 2-stage B ring
+    // (32 KB ring + 33 KB epilogue slab: 4 blocks = 4 waves/SIMD instead of 3 with 3 stages;
+    // the A operand's one-K-step register lookahead then meets its L2 latency: adapters' 3x3
+    // -8..10 %, YOLO adapter 1x1 -12 %, ViT fc1 -4 % in isolation, +0.2..0.4 % on the
+    // concurrent-heads bench), short-K or narrow precision-3 convs the 256x64 tile
     // PRPE_WAVE_WIDE=<tile> in the environment overrides the wide-shape choice (A/B runs)
     static const int wide = [] {
       const char* e = getenv("PRPE_WAVE_WIDE");
-      return e ? atoi(e) : 26;
+      return e ? atoi(e) : 28;
     }();
     // PRPE_WAVE_P3_NARROW=<tile> overrides the precision-3 short-K / narrow choice (A/B runs)
     static const int p3_narrow = [] {
@@ -392,9 +394,17 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       const char* e = getenv("PRPE_WAVE_P3_SMALLK");
       return e && e[0] == '0' ? 0 : 1;
     }();
+    static const int wide3 = [] {
+      const char* e = getenv("PRPE_WAVE_WIDE3");
+      return e ? atoi(e) : 27;
+    }();
+    static const int tile2 = [] {
+      const char* e = getenv("PRPE_WAVE_P2");
+      return e ? atoi(e) : 27;
+    }();
     if (prec == 0) tile = wide;
-    else if (prec == 3) tile = kp.Co > 64 && (kp.K > 128 || p3_smallk_wide) ? wide : p3_narrow;
-    else tile = kp.Co > 64 && kp.K > 128 ? 21 : 24;
+    else if (prec == 3) tile = kp.Co > 64 && (kp.K > 128 || p3_smallk_wide) ? wide3 : p3_narrow;
+    else tile = kp.Co > 64 && kp.K > 128 ? tile2 : 24;
   }
   if (prec == 0) {
     switch (tile) {
@@ -405,6 +415,8 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       case 25: return launch<8, 4, 8, 2, 2>(kp, st);   // 512 x 128, 2 stages
       case 26: return launch<4, 2, 8, 2, 3>(kp, st);   // 128 x 128, wave 32 x 128, 4 waves
       case 27: return launch<2, 4, 8, 2, 3>(kp, st);   // 128 x 128, wave 64 x 128, 2 waves
+      case 28: return launch<4, 2, 8, 2, 2>(kp, st);   // 128 x 128, wave 32 x 128, 2 stages
+      case 29: return launch<4, 4, 8, 2, 2>(kp, st);   // 256 x 128, wave 64 x 128, 2 stages
       default: return PRPE_EINVAL;
     }
   }
@@ -416,6 +428,7 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       case 24: return launch<4, 4, 8, 2, 3, true>(kp, st);
       case 25: return launch<8, 2, 4, 2, 3, true>(kp, st);   // 256 x 64, wave 32 x 64
       case 26: return launch<4, 2, 8, 2, 3, true>(kp, st);   // 128 x 128, wave 32 x 128, 4 waves
+      case 27: return launch<4, 2, 8, 2, 2, true>(kp, st);   // 128 x 128, 2 stages
       default: return PRPE_EINVAL;
     }
   }
@@ -426,6 +439,7 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
     case 24: return launch<8, 2, 4, 3, 3>(kp, st);   // 256 x 64,  wave 32 x 64
     case 25: return launch<8, 2, 8, 3, 2>(kp, st);   // 256 x 128, 2 stages
     case 26: return launch<4, 2, 8, 3, 3>(kp, st);   // = 21 (128 x 128, 4 waves)
+    case 27: return launch<4, 2, 8, 3, 2>(kp, st);   // 128 x 128, 4 waves, 2 stages
     default: return PRPE_EINVAL;
   }
 }

@@ -14,5 +14,5 @@ if [ "${PROF:-1}" = "1" ]; then
   export TMPDIR=/tmp
   timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o prof -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_$TAG.log 2>&1 || { tail -30 gpurun_out/prof_$TAG.log; exit 1; }
   DB=$(python -c "import glob,sys;print(sorted(glob.glob(sys.argv[1]+'/**/*.db',recursive=True))[0])" gpurun_out/prof_$TAG)
-  python tools/prof_summary.py $DB --passes 7 --dominant '%conv_wave_kernelILi4ELi2ELi8ELi2ELi3ELb0ELb0ELb0E%' --grid 25165824 > gpurun_out/prof_summary_$TAG.txt 2>&1; cat gpurun_out/prof_summary_$TAG.txt
+  python tools/prof_summary.py $DB --passes 7 --dominant '%conv_wave_kernelILi4ELi2ELi8ELi2ELi2ELb0ELb0ELb0E%' --grid 25165824 > gpurun_out/prof_summary_$TAG.txt 2>&1; cat gpurun_out/prof_summary_$TAG.txt
 fi
