@@ -663,12 +663,14 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     else hipLaunchKernelGGL((conv_smallco_kernel<4, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
     return launch_status();
   }
-  // direct global->LDS kernel (conv_glds.hip) for chunked inputs with Co > 32; tile 10..12
-  // forces one of its tiles. PRPE_CONV_GLDS=0 in the environment keeps every conv on this
-  // file's register-staged kernel (A/B measurements).
+  // direct global->LDS kernel (conv_glds.hip) for chunked inputs with Co > 32: tile 10..12
+  // forces one of its tiles; PRPE_CONV_GLDS=1 in the environment makes it the automatic
+  // choice for two-plane Co <= 64 convs again. Off by default: this file's 256x64 tile now
+  // measures 27 % faster on those shapes in isolation (profiles/r01_conv_bench_sweep_v4.txt)
+  // and -0.6..1.0 ms per sequential forward (AdaFace / YOLO adapter 64-channel convs).
   static const int glds_on = [] {
     const char* e = getenv("PRPE_CONV_GLDS");
-    return e && e[0] == '0' ? 0 : 1;
+    return e && e[0] == '1' ? 1 : 0;
   }();
   static const int wave_on = [] {
     const char* e = getenv("PRPE_CONV_WAVE");
@@ -682,8 +684,8 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   if (tile >= 20 || dual || d->x_planes || d->y_planes)
     return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile ? tile : 20, st) : PRPE_EINVAL;
   if (tile >= 10) return conv_glds_eligible(kp, prec, km) ? conv_glds_launch(kp, prec, tile, st) : PRPE_EINVAL;
-  // wave-row kernel everywhere it applies except two-plane Co <= 64, where the LDS-staged
-  // 256x64 tile measured faster (profiles/r01_conv_bench_wave.txt)
+  // wave-row kernel everywhere it applies except two-plane Co <= 64, where the register-staged
+  // 256x64 tile measured faster (profiles/r01_conv_bench_wave.txt, r01_conv_bench_sweep_v4.txt)
   if (tile == 0 && wave_on && y.c > 32 && (prec == 2 || y.c > 64) && conv_wave_eligible(kp, prec, km))
     return conv_wave_launch(kp, prec, 20, st);
   if (tile == 0 && glds_on && y.c > 32 && conv_glds_eligible(kp, prec, km)) return conv_glds_launch(kp, prec, 0, st);
