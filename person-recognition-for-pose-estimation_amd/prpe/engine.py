@@ -171,7 +171,7 @@ class Engine:
         if x_planes and prec != 0:
             raise RuntimeError(f"{p.name}: planes-format input needs precision 0, got {prec}")
         y_planes = PLANES_ON and planes_out and prec == 0 and p.co % 8 == 0 and out.is_contiguous()
-        kw = dict(res=res, res_mode=res_mode, act=act, precision=prec, x_amax=xa, y_amax=ya, x2=x2,
+        kw = dict(res=res, res_mode=res_mode, act=act, precision=prec, tile=p.tile, x_amax=xa, y_amax=ya, x2=x2,
                   x2_amax=x2_amax if prec == 3 else None, x_planes=x_planes, y_planes=y_planes)
         if p.name in self.watch:          # HIP events around one kernel (bench roofline)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -474,6 +474,10 @@ class Engine:
             s1, b1 = bn_affine(sd, m + ".output_layer.4", BN_EPS, sd[m + ".output_layer.3.bias"])
             in_s, in_b = bn_affine(sd, m + ".output_layer.0", BN_EPS)
             lin = pack_conv("ir50.output", w, 1, 0, self.device, scale=s1, bias=b1, in_scale=in_s, in_bias=in_b)
+            # M = frames (one output pixel each), K = 25,088: the automatic wave tile leaves 8
+            # blocks; the 128x16 register-staged tile runs 64 (bit-identical; PRPE_IR50_OUT_TILE=0
+            # restores the automatic choice; profiles/r01_conv_bench_ir50_output.txt)
+            lin.tile = int(os.environ.get("PRPE_IR50_OUT_TILE", "4"))
             self._packs["ir50.output"] = lin
         B = x.shape[0]
         y = self.conv(x, lin)                                # [B,1,1,512]

@@ -46,6 +46,7 @@ class ConvPack:
     act: str = "none"
     k_order: int = 0
     f16: tuple | None = None      # (w_h16, w_l16, scale16), built on first precision-3 use
+    tile: int = 0                 # kernel tile for prpe_conv2d (0 = the library's automatic choice)
 
     @property
     def flops_per_pixel(self) -> int:
