@@ -546,6 +546,9 @@ __global__ __launch_bounds__(256) void dfl_decode_kernel(DflK p) {
 // frames -> NHWC4 so the 7x7 stem takes the vectorised implicit-GEMM path)
 // (+ optional max|y| into *y_amax: the stem's precision-3 activation scale)
 struct CopyK { prpe_view x, y; int per_row, chunks; float* y_amax; };
+// Y4: y is 4 contiguous, 16-B aligned channels per pixel (the stem's NHWC4 buffer): one
+// 16-B store per pixel instead of four 4-B ones
+template <bool Y4>
 __global__ __launch_bounds__(256) void copy_pad_kernel(CopyK p) {
   int row, w;
   row_pos(p.chunks, row, w);
@@ -553,10 +556,20 @@ __global__ __launch_bounds__(256) void copy_pad_kernel(CopyK p) {
   if (w < p.per_row) {
     const int n = row / p.y.h, h = row - n * p.y.h;
     float* y = p.y.ptr + voff(p.y, n, h, w, 0);
-    for (int c = 0; c < p.y.c; ++c) {
-      const float v = c < p.x.c ? p.x.ptr[voff(p.x, n, h, w, c)] : 0.f;
-      y[(int64_t)c * p.y.sc] = v;
-      m = fmaxf(m, fabsf(v));
+    if constexpr (Y4) {
+      float v[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        v[c] = c < p.x.c ? p.x.ptr[voff(p.x, n, h, w, c)] : 0.f;
+        m = fmaxf(m, fabsf(v[c]));
+      }
+      *reinterpret_cast<float4*>(y) = make_float4(v[0], v[1], v[2], v[3]);
+    } else {
+      for (int c = 0; c < p.y.c; ++c) {
+        const float v = c < p.x.c ? p.x.ptr[voff(p.x, n, h, w, c)] : 0.f;
+        y[(int64_t)c * p.y.sc] = v;
+        m = fmaxf(m, fabsf(v));
+      }
     }
   }
   if (p.y_amax) amax_commit(p.y_amax, m);
@@ -668,7 +681,10 @@ extern "C" int prpe_copy_pad(const prpe_view* x, const prpe_view* y, float* y_am
   CopyK p{*x, *y, y->w, 0, y_amax};
   dim3 g;
   if (!rowgrid((int64_t)y->n * y->h, y->w, g, p.chunks)) return PRPE_EINVAL;
-  hipLaunchKernelGGL(copy_pad_kernel, g, dim3(256), 0, as_stream(stream), p);
+  const bool y4 = y->c == 4 && y->sc == 1 && y->sw % 4 == 0 && y->sh % 4 == 0 && y->sn % 4 == 0 &&
+                  (uintptr_t)y->ptr % 16 == 0;
+  if (y4) hipLaunchKernelGGL(copy_pad_kernel<true>, g, dim3(256), 0, as_stream(stream), p);
+  else hipLaunchKernelGGL(copy_pad_kernel<false>, g, dim3(256), 0, as_stream(stream), p);
   return launch_status();
 }
 

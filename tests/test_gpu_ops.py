@@ -740,3 +740,23 @@ def test_dfl_decode_matches_oracle_head(stride):
     a1, b1 = anchors.unsqueeze(0) - lt, anchors.unsqueeze(0) + rb
     ref = torch.cat((torch.cat(((a1 + b1) / 2, b1 - a1), 1) * strides, cls.sigmoid()), 1)
     torch.testing.assert_close(det.cpu(), ref, rtol=2e-6, atol=2e-5)
+
+
+@pytest.mark.parametrize("yc,flip", [(4, False), (4, True), (5, False), (8, True)])
+def test_copy_pad_nchw_to_padded_nhwc(yc, flip):
+    """prpe_copy_pad: NCHW frames (read in place through a permuted view) into the interior of a
+    zero-bordered NHWC buffer with yc >= 3 channels (4 = the stem's NHWC4 buffer: one 16-B
+    store per pixel), optionally mirrored along W, raising max|y|. Exact copy."""
+    x = torch.randn(2, 3, 13, 21)
+    buf = torch.full((2, 13 + 6, 21 + 8, yc), 7.0, device=DEV)
+    y = buf[:, 3:3 + 13, 4:4 + 21, :]
+    ya = torch.zeros(1, device=DEV)
+    ops.copy_pad(x.to(DEV).permute(0, 2, 3, 1), y, flip_w=flip, y_amax=ya)
+    torch.cuda.synchronize()
+    ref = x.flip(3) if flip else x
+    got = y.cpu()
+    assert torch.equal(got[..., :3], ref.permute(0, 2, 3, 1))
+    assert torch.equal(got[..., 3:], torch.zeros_like(got[..., 3:]))
+    assert ya.item() == x.abs().max().item()
+    # the border is untouched
+    assert torch.equal(buf[:, :3].cpu(), torch.full_like(buf[:, :3].cpu(), 7.0))
