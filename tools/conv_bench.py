@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--korders", default="0,1", help="weight K orders to compare (1 = chunk-major)")
     ap.add_argument("--amax", action="store_true", help="also track max|y| (y_amax) in the epilogue")
+    ap.add_argument("--act", default="relu", help="epilogue activation (relu, gelu, silu, prelu, none)")
     ap.add_argument("--planes", action="store_true",
                     help="input in the planes format (x_planes; precision 0, wave-row kernel)")
     a = ap.parse_args()
@@ -67,7 +68,7 @@ def main():
         for ko in [int(v) for v in a.korders.split(",")]:
             if ko == 1 and (k == 1 or Ci % 32):
                 continue
-            pks[ko] = pack.pack_conv("b", w, s, p, dev, scale=torch.ones(Co), bias=torch.zeros(Co), act="relu",
+            pks[ko] = pack.pack_conv("b", w, s, p, dev, scale=torch.ones(Co), bias=torch.zeros(Co), act=a.act,
                                      k_order=ko)
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         y = torch.empty(B, Ho, Wo, Co, device=dev)
