@@ -272,6 +272,38 @@ def test_conv_wave_kernel_bit_exact_vs_lds_staged(B, Ci, H, W, Co, k, s, p, tile
     torch.testing.assert_close(got, ref, rtol=0, atol=_tol(x, w) * 2)
 
 
+@pytest.mark.parametrize("precision,tile", [(0, 28), (0, 29), (2, 27)])
+@pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", WAVE_SHAPES)
+def test_conv_wave_two_stage_ring_bit_exact(B, Ci, H, W, Co, k, s, p, tile, precision):
+    """The 2-stage B-ring tiles (the automatic wide choice for precision 0 / 2): same K order, plane split and MFMA order per accumulator as the register-staged
+    kernel, so bit-identical to it; pre-activation residual included."""
+    x = rnd(B, Ci, H, W, seed=80)
+    w = rnd(Co, Ci, k, k, seed=81, scale=1.0 / math.sqrt(Ci * k * k))
+    sc = torch.rand(Co, generator=_g(82)) + 0.5
+    bi = rnd(Co, seed=83)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    # (a 1x1-pixel residual permuted to NHWC keeps unit W/H strides, which the vector epilogue
+    # rightly rejects; that shape runs without one)
+    r = rnd(B, Co, Ho, Wo, seed=97) if Ho * Wo > 1 else None
+    kw = dict(act="gelu", scale=sc, bias=bi, k_order=1, precision=precision, res=r,
+              res_mode=RES_PRE if r is not None else 0)
+    got = run_conv(x, w, s, p, tile=tile, **kw)
+    assert torch.equal(got, run_conv(x, w, s, p, tile=5, **kw))
+
+
+@pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", WAVE_SHAPES)
+def test_conv_f16_two_stage_ring_bit_exact(B, Ci, H, W, Co, k, s, p):
+    """precision 3: the 2-stage 128x128 tile (27, the automatic wide choice) agrees bit for bit
+    with the 3-stage one (26)."""
+    x = torch.relu(rnd(B, Ci, H, W, seed=91)) * 7.0
+    w = rnd(Co, Ci, k, k, seed=92, scale=1.0 / math.sqrt(Ci * k * k))
+    sc = torch.rand(Co, generator=_g(93)) + 0.5
+    bi = rnd(Co, seed=94)
+    a, ya = _conv_p3(x, w, s, p, tile=27, scale=sc, bias=bi, act="silu")
+    b, yb = _conv_p3(x, w, s, p, tile=26, scale=sc, bias=bi, act="silu")
+    assert torch.equal(a, b) and ya == yb
+
+
 @pytest.mark.parametrize("mode", [RES_PRE, RES_POST])
 @pytest.mark.parametrize("tile", [21, 23])
 def test_conv_wave_kernel_prologue_residual_prelu(mode, tile):
