@@ -380,43 +380,85 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(Up2K p) {
 
 // ------------------------------------------------------------------------- norm_sigmoid
 // one workgroup per sample; channels <= 4; double accumulation (two passes)
-__global__ __launch_bounds__(256) void norm_sigmoid_kernel(prpe_view x, prpe_view y) {
+// One block of NS_T threads per sample; every pass covers all C <= 4 channels at once (a
+// pixel's channels are adjacent in NHWC): sums, centred sums, then normalise + sigmoid. The
+// pixel walk is incremental (no per-element division). Partial sums in fp64, as before.
+constexpr int NS_T = 1024;
+__global__ __launch_bounds__(NS_T) void norm_sigmoid_kernel(prpe_view x, prpe_view y) {
+  constexpr int NWV = NS_T / 64;
   const int n = blockIdx.x;
-  const int C = x.c, HW = x.h * x.w;
-  __shared__ double red[4][4];
+  const int C = x.c, W = x.w, HW = x.h * x.w;
+  __shared__ double red[NWV][8];
   __shared__ float stat[4][2];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int c = 0; c < C; ++c) {
-    double s = 0.0;
-    for (int i = threadIdx.x; i < HW; i += blockDim.x) s += x.ptr[voff(x, n, i / x.w, i % x.w, c)];
-    s = warp_sum_d(s);
-    if (lane == 0) red[wave][0] = s;
-    __syncthreads();
-    const float mean = (float)((red[0][0] + red[1][0] + red[2][0] + red[3][0]) / HW);
-    __syncthreads();
-    // std of the centred values (modify_models.py:84-85): unbiased, around their own mean
-    double s1 = 0.0, s2 = 0.0;
-    for (int i = threadIdx.x; i < HW; i += blockDim.x) {
-      const double d = (double)(x.ptr[voff(x, n, i / x.w, i % x.w, c)] - mean);
-      s1 += d; s2 += d * d;
-    }
-    s1 = warp_sum_d(s1); s2 = warp_sum_d(s2);
-    if (lane == 0) { red[wave][1] = s1; red[wave][2] = s2; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const double S1 = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-      const double S2 = red[0][2] + red[1][2] + red[2][2] + red[3][2];
-      const double var = (S2 - S1 * S1 / HW) / (HW - 1);
-      stat[c][0] = mean;
-      stat[c][1] = (float)sqrt(var > 0.0 ? var : 0.0);
-    }
-    __syncthreads();
+  const float* xn = x.ptr + (int64_t)n * x.sn;
+  const int h0 = (int)threadIdx.x / W, w0 = (int)threadIdx.x - h0 * W;
+  const int dh = NS_T / W, dw = NS_T - dh * W;                 // dw < W: at most one carry
+  // pass 1: per-channel sums -> means
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i = threadIdx.x, h = h0, w = w0; i < HW; i += NS_T) {
+    const float* px = xn + (int64_t)h * x.sh + (int64_t)w * x.sw;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < C) s[c] += px[(int64_t)c * x.sc];
+    w += dw; h += dh;
+    if (w >= W) { w -= W; ++h; }
   }
-  for (int i = threadIdx.x; i < HW * C; i += blockDim.x) {
-    const int c = i % C, pix = i / C;
-    const int h = pix / x.w, w = pix % x.w;
-    const float v = (x.ptr[voff(x, n, h, w, c)] - stat[c][0]) / (stat[c][1] + 1e-6f);
-    y.ptr[voff(y, n, h, w, c)] = 1.f / (1.f + expf(-v));
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const double t = warp_sum_d(s[c]);
+    if (lane == 0) red[wave][c] = t;
+  }
+  __syncthreads();
+  float mean[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    double t = 0.0;
+    for (int v = 0; v < NWV; ++v) t += red[v][c];
+    mean[c] = (float)(t / HW);
+  }
+  __syncthreads();
+  // pass 2: std of the centred values (modify_models.py:84-85): unbiased, around their own mean
+  double s1[4] = {0.0, 0.0, 0.0, 0.0}, s2[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i = threadIdx.x, h = h0, w = w0; i < HW; i += NS_T) {
+    const float* px = xn + (int64_t)h * x.sh + (int64_t)w * x.sw;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < C) {
+        const double d = (double)(px[(int64_t)c * x.sc] - mean[c]);
+        s1[c] += d; s2[c] += d * d;
+      }
+    w += dw; h += dh;
+    if (w >= W) { w -= W; ++h; }
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const double t1 = warp_sum_d(s1[c]), t2 = warp_sum_d(s2[c]);
+    if (lane == 0) { red[wave][c] = t1; red[wave][4 + c] = t2; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 4 && (int)threadIdx.x < C) {
+    const int c = threadIdx.x;
+    double S1 = 0.0, S2 = 0.0;
+    for (int v = 0; v < NWV; ++v) { S1 += red[v][c]; S2 += red[v][4 + c]; }
+    const double var = (S2 - S1 * S1 / HW) / (HW - 1);
+    stat[c][0] = mean[c];
+    stat[c][1] = (float)sqrt(var > 0.0 ? var : 0.0);
+  }
+  __syncthreads();
+  // pass 3: normalise + sigmoid
+  float* yn = y.ptr + (int64_t)n * y.sn;
+  for (int i = threadIdx.x, h = h0, w = w0; i < HW; i += NS_T) {
+    const float* px = xn + (int64_t)h * x.sh + (int64_t)w * x.sw;
+    float* py = yn + (int64_t)h * y.sh + (int64_t)w * y.sw;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < C) {
+        const float v = (px[(int64_t)c * x.sc] - stat[c][0]) / (stat[c][1] + 1e-6f);
+        py[(int64_t)c * y.sc] = 1.f / (1.f + expf(-v));
+      }
+    w += dw; h += dh;
+    if (w >= W) { w -= W; ++h; }
   }
 }
 
@@ -719,7 +761,7 @@ extern "C" int prpe_norm_sigmoid(const prpe_view* x, const prpe_view* y, void* s
   if (!view_ok(x) || !view_ok(y) || x->c > 4 || x->c != y->c || x->n != y->n || x->h != y->h || x->w != y->w ||
       x->h * x->w < 2)
     return PRPE_EINVAL;
-  hipLaunchKernelGGL(norm_sigmoid_kernel, dim3(x->n), dim3(256), 0, as_stream(stream), *x, *y);
+  hipLaunchKernelGGL(norm_sigmoid_kernel, dim3(x->n), dim3(NS_T), 0, as_stream(stream), *x, *y);
   return launch_status();
 }
 

@@ -688,6 +688,24 @@ def test_upsample_nearest2x():
                                rtol=0, atol=0)
 
 
+@pytest.mark.parametrize("B,C,H,W,nchw_out", [(2, 3, 160, 160, False), (2, 1, 3, 1100, True), (1, 4, 33, 31, True),
+                                              (2, 2, 1, 2, False)])
+def test_norm_sigmoid_shapes(B, C, H, W, nchw_out):
+    """Per-sample per-channel standardisation + sigmoid (modify_models.py:84-86) at the model's
+    160x160, rows wider than one block (W > 1024), ragged sizes, C = 1..4, NCHW output view."""
+    x = rnd(B, C, H, W, seed=39, scale=3.0) + 0.7
+    if nchw_out:
+        yb = torch.empty(B, C, H, W, device=DEV)
+        y = yb.permute(0, 2, 3, 1)
+    else:
+        y = torch.empty(B, H, W, C, device=DEV)
+    ops.norm_sigmoid(x.permute(0, 2, 3, 1).contiguous().to(DEV), y)
+    torch.cuda.synchronize()
+    r = x.double() - x.double().mean(dim=(2, 3), keepdim=True)
+    r = torch.sigmoid(r / (r.std(dim=(2, 3), keepdim=True) + 1e-6)).float()
+    torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), r, rtol=0, atol=2e-6)
+
+
 def test_norm_sigmoid():
     x = rnd(3, 3, 40, 40, seed=38, scale=3.0) + 0.7
     y = torch.empty(3, 40, 40, 3, device=DEV)
