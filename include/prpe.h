@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PRPE_ABI_VERSION 3
+#define PRPE_ABI_VERSION 4
 
 /* activations (epilogues/prologues) */
 enum prpe_act {
@@ -94,19 +94,20 @@ typedef struct prpe_conv_desc {
                              (register-staged); 10..12 LDS-DMA staged; 21..25 wave-row */
   int32_t k_order;        /* weight K order, see above */
   /* precision 3 operands: fp16 planes [co_pad][k_pad] of w[co][k] * 2^e[co] (w = (h16 + l16)
-   * * 2^-e[co] to ~2^-22), the epilogue scale with 2^-e[co] folded in, and a device scalar
-   * bounding max|x| (the producer's y_amax) that sets the activations' power-of-2 scale */
+   * * 2^-e[co] to ~2^-22), the epilogue scale with 2^-e[co] folded in, and PER-FRAME bounds
+   * x_amax[n] >= max|x[n]| (n < N; the producer's y_amax) that set each frame's power-of-2
+   * activation scale -- a frame's arithmetic never depends on the other frames of the batch */
   const uint16_t* w_h16;
   const uint16_t* w_l16;
   const float* scale16;   /* [Co] */
-  const float* x_amax;
-  float* y_amax;          /* optional (any precision): device scalar raised to max|y| (atomic;
-                             zero it before the producing launch) */
+  const float* x_amax;    /* [N] device */
+  float* y_amax;          /* optional (any precision): device [N], y_amax[n] raised to max|y[n]|
+                             (atomic; zero it before the producing launch) */
   /* optional second input (x2.ptr != NULL): y = EPI(W[:, :Ci] x + W[:, Ci:] x2), a 1x1 unpadded
    * conv over both; x2 is [N, Ho, Wo, C2] on the output's pixel grid (any strides, e.g. a
    * stride-2 subsampling view), channel-contiguous, C2 % 32 == 0 and Ci % 32 == 0; weights
-   * packed [co_pad][k_pad] with k = Ci + C2 columns; precision 0/2/3 (3 also needs x2_amax;
-   * one activation scale for both inputs). Replaces a ResNet bottleneck's conv3 + downsample
+   * packed [co_pad][k_pad] with k = Ci + C2 columns; precision 0/2/3 (3 also needs x2_amax [N];
+   * one activation scale per frame for both inputs). Replaces a ResNet bottleneck's conv3 + downsample
    * projection + residual add (torchvision resnet50 Bottleneck.forward) with one GEMM. */
   prpe_view x2;
   const float* x2_amax;
@@ -154,7 +155,8 @@ int prpe_maxpool(const prpe_view* x, const prpe_view* y, int32_t k, int32_t stri
                  int32_t pad, void* stream);
 
 /* Strided copy with channel zero-padding: y[...,c] = c < x.c ? x[...,c] : 0 (e.g. NCHW frames
- * -> NHWC4 for the vectorised stem conv; the 4th channel meets a zero weight column). */
+ * -> NHWC4 for the vectorised stem conv; the 4th channel meets a zero weight column).
+ * y_amax (optional): device [N], y_amax[n] raised to max|y[n]| (zeroed by the caller). */
 int prpe_copy_pad(const prpe_view* x, const prpe_view* y, float* y_amax /* optional */, void* stream);
 
 /* Nearest x2 upsample (yolopt DarkFPN nn.Upsample(scale_factor=2), nn.py:195). */
@@ -191,8 +193,10 @@ int prpe_dfl_decode(const float* head, float* out, int32_t B, int32_t nc, int32_
                     const int32_t* level_hw /* [nlevels*2] host */, const float* strides /* host */,
                     void* stream);
 
-/* Row-wise L2 normalisation: norm = ||x||_2, emb = x / norm (net_adaface.py:334-337). */
-int prpe_l2norm(const float* x, float* emb, float* norm, int32_t rows, int32_t C, void* stream);
+/* Row-wise L2 normalisation: norm = ||x||_2, emb = x / max(norm, eps).
+ * eps = 0: IR-50 output torch.div(x, norm) (net_adaface.py:334-337; a zero row gives NaN as there);
+ * eps = 1e-12: F.normalize (face_recognition/module.py:137-138; a zero row gives 0). */
+int prpe_l2norm(const float* x, float* emb, float* norm, int32_t rows, int32_t C, float eps, void* stream);
 
 /*
  * yolopt.util.non_max_suppression (training/yolopt/util.py:123-169), batched, on device.

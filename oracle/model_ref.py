@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import math
 
+import numpy as np
 import torch
 import torch.nn.functional as F
 
@@ -312,11 +313,51 @@ def forward_all(sd, x, stride=(8.0, 16.0, 32.0), calib=None):
 
 
 # ----------------------------------------------------------------------------- post-proc
-def nms_single(boxes: Tensor, scores: Tensor, thr: float) -> Tensor:
+def nms_restated(boxes: Tensor, scores: Tensor, iou_threshold: float, max_keep: int | None = None) -> Tensor:
+    """torchvision.ops.nms semantics (CPU kernel), restated in numpy float32.
+
+    Greedy: visit boxes by descending score; keep a box unless an already-kept box
+    has IoU > thr with it; IoU = inter / (area_i + area_j - inter), all in float32.
+    Ties: torchvision sorts with ``scores.sort(descending=True)`` whose CPU order for
+    equal scores is unspecified (not stable above ~16 elements); this restatement breaks
+    ties by index (stable), which is the contract of the HIP kernel too.
+    ``max_keep``: stop after that many kept boxes -- the greedy pass is sequential in score
+    order, so the first max_keep kept indices are the same as the full result's.
+    """
+    b = boxes.detach().cpu().numpy().astype(np.float32)
+    s = scores.detach().cpu().numpy().astype(np.float32)
+    n = b.shape[0]
+    if n == 0:
+        return torch.zeros(0, dtype=torch.int64)
+    order = np.argsort(-s, kind="stable")
+    x1, y1, x2, y2 = (b[order, i] for i in range(4))
+    areas = (x2 - x1) * (y2 - y1)
+    alive = np.ones(n, dtype=bool)
+    keep = []
+    for i in range(n):
+        if not alive[i]:
+            continue
+        keep.append(order[i])
+        if max_keep is not None and len(keep) >= max_keep:
+            break
+        j = np.arange(i + 1, n)
+        j = j[alive[i + 1:]]
+        if j.size == 0:
+            break
+        xx1 = np.maximum(x1[i], x1[j]); yy1 = np.maximum(y1[i], y1[j])
+        xx2 = np.minimum(x2[i], x2[j]); yy2 = np.minimum(y2[i], y2[j])
+        w = np.maximum(np.float32(0), xx2 - xx1); h = np.maximum(np.float32(0), yy2 - yy1)
+        inter = w * h
+        with np.errstate(divide="ignore", invalid="ignore"):
+            ovr = inter / (areas[i] + areas[j] - inter)
+        alive[j[ovr > np.float32(iou_threshold)]] = False
+    return torch.as_tensor(np.array(keep, dtype=np.int64))
+
+
+def nms_single(boxes: Tensor, scores: Tensor, thr: float, max_keep: int | None = None) -> Tensor:
     """torchvision.ops.nms semantics (CPU kernel), called at yolopt/util.py:162:
     stable descending score order, suppress j iff IoU(i, j) > thr."""
-    from oracle.ref_shims import nms_restated
-    return nms_restated(boxes, scores, thr)
+    return nms_restated(boxes, scores, thr, max_keep)
 
 
 def non_max_suppression(outputs: Tensor, confidence_threshold=0.001, iou_threshold=0.65):
@@ -349,7 +390,7 @@ def non_max_suppression(outputs: Tensor, confidence_threshold=0.001, iou_thresho
         # leaves tie order unspecified; identical for tie-free scores)
         x = x[torch.sort(x[:, 4], descending=True, stable=True)[1][:max_nms]]
         c = x[:, 5:6] * max_wh
-        keep = nms_single(x[:, :4] + c, x[:, 4], iou_threshold)[:max_det]
+        keep = nms_single(x[:, :4] + c, x[:, 4], iou_threshold, max_det)[:max_det]
         out[i] = x[keep]
     return out
 

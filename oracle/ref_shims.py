@@ -88,41 +88,9 @@ def _resnet50(pretrained=False, **kw):  # pretrained weights need the network: i
     return _ResNet50()
 
 
-def nms_restated(boxes: torch.Tensor, scores: torch.Tensor, iou_threshold: float) -> torch.Tensor:
-    """torchvision.ops.nms semantics (CPU kernel), restated in numpy float32.
-
-    Greedy: visit boxes by descending score; keep a box unless an already-kept box
-    has IoU > thr with it; IoU = inter / (area_i + area_j - inter), all in float32.
-    Ties: torchvision sorts with ``scores.sort(descending=True)`` whose CPU order for
-    equal scores is unspecified (not stable above ~16 elements); this restatement breaks
-    ties by index (stable), which is the contract of the HIP kernel too.
-    """
-    b = boxes.detach().cpu().numpy().astype(np.float32)
-    s = scores.detach().cpu().numpy().astype(np.float32)
-    n = b.shape[0]
-    if n == 0:
-        return torch.zeros(0, dtype=torch.int64)
-    order = np.argsort(-s, kind="stable")
-    x1, y1, x2, y2 = (b[order, i] for i in range(4))
-    areas = (x2 - x1) * (y2 - y1)
-    alive = np.ones(n, dtype=bool)
-    keep = []
-    for i in range(n):
-        if not alive[i]:
-            continue
-        keep.append(order[i])
-        j = np.arange(i + 1, n)
-        j = j[alive[i + 1:]]
-        if j.size == 0:
-            break
-        xx1 = np.maximum(x1[i], x1[j]); yy1 = np.maximum(y1[i], y1[j])
-        xx2 = np.minimum(x2[i], x2[j]); yy2 = np.minimum(y2[i], y2[j])
-        w = np.maximum(np.float32(0), xx2 - xx1); h = np.maximum(np.float32(0), yy2 - yy1)
-        inter = w * h
-        with np.errstate(divide="ignore", invalid="ignore"):
-            ovr = inter / (areas[i] + areas[j] - inter)
-        alive[j[ovr > np.float32(iou_threshold)]] = False
-    return torch.as_tensor(np.array(keep, dtype=np.int64))
+# torchvision.ops.nms: restated in oracle/model_ref.py (the oracle ships to the GPU box; this
+# container-only shim module does not)
+from oracle.model_ref import nms_restated  # noqa: E402
 
 
 def _stub(name, **attrs):

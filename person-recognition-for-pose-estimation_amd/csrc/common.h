@@ -84,17 +84,56 @@ __device__ __forceinline__ float amax4(f32x4 v) {
 }
 // raise *slot to the wave's maximum of m (m >= 0: float order == unsigned bit order); every
 // lane of the wave must call it
+__device__ __forceinline__ void amax_raise(float* slot, float m) {
+  // the slot only grows, so read it first (an agent-scope load, past the non-coherent L1) and
+  // only raise it when m is larger -- a stale read can only cost a redundant atomic
+  unsigned* u = reinterpret_cast<unsigned*>(slot);
+  const unsigned b = __float_as_uint(m);
+  if (b > __hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(u, b);
+}
 __device__ __forceinline__ void amax_commit(float* slot, float m) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0 && m > 0.f) {
-    // one slot per tensor, so most waves would contend on one address: read it first (an
-    // agent-scope load, past the non-coherent L1) and only raise it when this wave's max is
-    // larger -- the slot only grows, so a stale read can only cost a redundant atomic
-    unsigned* u = reinterpret_cast<unsigned*>(slot);
-    const unsigned b = __float_as_uint(m);
-    if (b > __hip_atomic_load(u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(u, b);
+  if ((threadIdx.x & 63) == 0 && m > 0.f) amax_raise(slot, m);
+}
+
+// Per-FRAME max|y| (prpe.h, "max|y| slots"): slots[n] bounds |y| over frame n only, so a
+// frame's precision-3 scale never depends on its batch-mates. A lane visits its rows in
+// increasing order and keeps (frame, running max); when its frame changes it raises the old
+// frame's slot itself. frame_amax_final: when every lane with a maximum is on the same frame
+// (a wave inside one frame: the common case) one wave reduction and one atomic, else one
+// atomic per lane. Every lane of the wave must call it.
+struct FrameMax {
+  int n = -1;
+  float m = 0.f;
+  __device__ __forceinline__ void add(float* slots, int frame, float v) {
+    if (frame != n) {
+      if (n >= 0 && m > 0.f) amax_raise(slots + n, m);
+      n = frame;
+      m = 0.f;
+    }
+    m = fmaxf(m, v);
   }
+};
+__device__ __forceinline__ void frame_amax_final(float* slots, FrameMax f) {
+  int nmax = f.m > 0.f ? f.n : -1;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nmax = max(nmax, __shfl_xor(nmax, o, 64));
+  if (nmax < 0) return;
+  if (__all(f.m <= 0.f || f.n == nmax)) {
+    amax_commit(slots + nmax, f.m > 0.f ? f.m : 0.f);
+  } else if (f.n >= 0 && f.m > 0.f) {
+    amax_raise(slots + f.n, f.m);
+  }
+}
+
+// precision-3 activation scale of one frame: max|x| < 2^e -> x 2^(15-e) (e clamped; an
+// all-zero frame takes e = 15, scale 1). Both the operand split and the epilogue's inverse
+// derive from this one function, so they agree exactly.
+__device__ __forceinline__ int f16_scale_exp(float amax) {
+  int e = 0;
+  (void)frexpf(amax, &e);
+  return amax > 0.f ? (e < -60 ? -60 : (e > 60 ? 60 : e)) : 15;
 }
 
 // F = {0,2,3,1} indexed by (row >> 2) & 3, branch-free

@@ -181,7 +181,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_glds_kernel(ConvK p) {
   // ---------------- epilogue (as conv_igemm.hip): C tile staged through LDS, whole-row
   // 16-B column chunks per thread, coalesced residual loads and output stores
   float* ct = reinterpret_cast<float*>(lds);
-  float ymax = 0.f;                            // running max|y| (p.y_amax)
+  FrameMax ymax;                               // per-frame running max|y| (p.y_amax)
   constexpr int CPR = BN / 4;
   constexpr int RPP = NT / CPR;
   const int cc = tid % CPR;
@@ -210,6 +210,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_glds_kernel(ConvK p) {
         int64_t yo[EB];
         f4 res[EB];
         bool ok[EB];
+        int fn[EB];
 #pragma unroll
         for (int e = 0; e < EB; ++e) {
           const int rr = rb + RPP * e;
@@ -217,8 +218,10 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_glds_kernel(ConvK p) {
           ok[e] = rr < rows && m < p.M;
           res[e] = f4{0.f, 0.f, 0.f, 0.f};
           yo[e] = 0;
+          fn[e] = 0;
           if (ok[e]) {
             const int n = m / p.HoWo;
+            fn[e] = n;
             const int rem = m - n * p.HoWo;
             const int oh = rem / p.Wo;
             const int ow = rem - oh * p.Wo;
@@ -238,13 +241,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_glds_kernel(ConvK p) {
           for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
           if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
           *reinterpret_cast<f4*>(p.y + yo[e]) = v;
-          ymax = fmaxf(ymax, amax4(v));
+          if (p.y_amax) ymax.add(p.y_amax, fn[e], amax4(v));
         }
       }
     }
     if (h0 + CH < BM) __syncthreads();
   }
-  if (p.y_amax) amax_commit(p.y_amax, ymax);
+  if (p.y_amax) frame_amax_final(p.y_amax, ymax);
 }
 
 template <int BM, int BN, int NW, int NP2_STAGES, int NP3_STAGES>

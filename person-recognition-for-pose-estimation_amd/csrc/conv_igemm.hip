@@ -339,7 +339,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
   }
 
   // ---------------- epilogue
-  float ymax = 0.f;                                   // running max|y| (p.y_amax)
+  FrameMax ymax;                                      // per-frame running max|y| (p.y_amax)
   if (p.vec_out) {
     // Stage the raw accumulator tile through LDS (CH rows per round), then every thread owns
     // 16-B column chunks of whole rows: coalesced float4 residual loads and output stores.
@@ -375,6 +375,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
           int64_t yo[EB];
           f4 res[EB];
           bool ok[EB];
+          int fn[EB];
 #pragma unroll
           for (int e = 0; e < EB; ++e) {
             const int rr = rb + RPP * e;
@@ -382,8 +383,10 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
             ok[e] = rr < rows && m < p.M;
             res[e] = f4{0.f, 0.f, 0.f, 0.f};
             yo[e] = 0;
+            fn[e] = 0;
             if (ok[e]) {
               const int n = m / p.HoWo;
+              fn[e] = n;
               const int rem = m - n * p.HoWo;
               const int oh = rem / p.Wo;
               const int ow = rem - oh * p.Wo;
@@ -403,13 +406,13 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
             for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
             if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
             *reinterpret_cast<f4*>(p.y + yo[e]) = v;
-            ymax = fmaxf(ymax, amax4(v));
+            if (p.y_amax) ymax.add(p.y_amax, fn[e], amax4(v));
           }
         }
       }
       if (h0 + CH < BM) __syncthreads();
     }
-    if (p.y_amax) amax_commit(p.y_amax, ymax);
+    if (p.y_amax) frame_amax_final(p.y_amax, ymax);
     return;
   }
   float sc[TN], bi[TN], sl[TN];
@@ -444,11 +447,11 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void conv_igemm_kernel(ConvK p) {
         v = apply_act(v, p.act, sl[j]);
         if (p.res_mode == PRPE_RES_POST_ACT) v += p.r[ro + col * p.rsc];
         p.y[yo + col * p.ysc] = v;
-        ymax = fmaxf(ymax, fabsf(v));
+        if (p.y_amax) ymax.add(p.y_amax, n, fabsf(v));
       }
     }
   }
-  if (p.y_amax) amax_commit(p.y_amax, ymax);
+  if (p.y_amax) frame_amax_final(p.y_amax, ymax);
 }
 
 // Direct fp32 conv for Co <= 4 (ViT adapter 128->3, YOLO adapter 64->3, head 80->1): a 16-wide
@@ -480,7 +483,7 @@ __global__ __launch_bounds__(256) void conv_smallco_kernel(ConvK p, int lpp_log2
         }
         w[t][e][c] = v;
       }
-  float ymax = 0.f;
+  FrameMax ymax;
   const int gw = (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
   const int nw = (int)((gridDim.x * blockDim.x) >> 6);
   for (int base = gw * ppw; base < p.M; base += nw * ppw) {
@@ -522,11 +525,11 @@ __global__ __launch_bounds__(256) void conv_smallco_kernel(ConvK p, int lpp_log2
         v = apply_act(v, p.act, p.slope ? p.slope[c] : 0.f);
         if (p.res_mode == PRPE_RES_POST_ACT) v += p.r[ro + c * p.rsc];
         p.y[yo + c * p.ysc] = v;
-        ymax = fmaxf(ymax, fabsf(v));
+        if (p.y_amax) ymax.add(p.y_amax, n, fabsf(v));
       }
     }
   }
-  if (p.y_amax) amax_commit(p.y_amax, ymax);
+  if (p.y_amax) frame_amax_final(p.y_amax, ymax);
 }
 
 template <int BM, int BN, int WM, int WN, int KM, bool PRO>

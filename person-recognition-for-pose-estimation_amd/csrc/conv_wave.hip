@@ -39,8 +39,9 @@ constexpr int BK = 32;
 
 // F16 (precision 3): two fp16 planes instead of bf16 ones. The weights arrive pre-scaled per
 // output channel (2^e[co], folded back through the epilogue scale); the activations are
-// scaled by sa = 2^(15 - e) with max|x| < 2^e read from the producer's running maximum
-// (*x_amax), so every scaled value is < 2^15 and the planes stay inside fp16's range: operand
+// scaled by sa = 2^(15 - e) with max|x| < 2^e read from the producer's running maximum of
+// the row's frame (x_amax[n], per-frame slots: a frame's rounding never depends on its
+// batch-mates), so every scaled value is < 2^15 and the planes stay inside fp16's range: operand
 // error ~2^-22, below fp32's own accumulation error for K >= 64 (Precision).
 // DUAL: two 1x1 inputs summed in one GEMM, y = EPI(W[:, :K1] x + W[:, K1:] x2) (a ResNet
 // bottleneck's conv3 and its downsample projection: the projection is never written to HBM
@@ -77,14 +78,22 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   int64_t rbase[TM];
   int64_t rbase2[DUAL ? TM : 1];
   unsigned hmask[TM], wmask[TM];
+  float sa[F16 ? TM : 1];                             // precision 3: per-row (= per-frame) scale
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wrow0 + i * 16 + fr;
     unsigned hm = 0, wmk = 0;
     int64_t b = 0;
     if constexpr (DUAL) rbase2[i] = 0;
+    if constexpr (F16) sa[i] = 1.f;
     if (m < p.M) {
       const int n = m / p.HoWo;
+      if constexpr (F16) {
+        // activation scale of this row's frame: max|x| < 2^e -> 2^(15 - e); a dual GEMM's two
+        // inputs share one scale (their per-frame maxima combined)
+        const float am = DUAL ? fmaxf(p.x_amax[n], p.x2_amax[n]) : p.x_amax[n];
+        sa[i] = ldexpf(1.f, 15 - f16_scale_exp(am));
+      }
       const int rem = m - n * p.HoWo;
       const int oh = rem / p.Wo;
       const int ow = rem - oh * p.Wo;
@@ -159,16 +168,6 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     }
   };
 
-  // activation scale of the fp16 planes (wave-uniform): max|x| < 2^e -> sa = 2^(15 - e)
-  float sa = 1.f, inv_sa = 1.f;
-  if constexpr (F16) {
-    const float amax = DUAL ? fmaxf(*p.x_amax, *p.x2_amax) : *p.x_amax;   // one scale for both inputs
-    int e = 0;
-    (void)frexpf(amax, &e);
-    e = amax > 0.f ? (e < -60 ? -60 : (e > 60 ? 60 : e)) : 15;
-    sa = ldexpf(1.f, 15 - e);
-    inv_sa = ldexpf(1.f, e - 15);
-  }
   frag_t af[NP][TM];
   auto split_a = [&]() {
 #pragma unroll
@@ -184,8 +183,8 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
         af[1][i] = __builtin_bit_cast(bf16x8, v1);
       } else if constexpr (F16) {
         unsigned long long p0[2], p1[2];
-        split_planes_f16(v0, sa, p0);
-        split_planes_f16(v1, sa, p1);
+        split_planes_f16(v0, sa[i], p0);
+        split_planes_f16(v1, sa[i], p1);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -263,7 +262,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     if (p.bias) bi4 = *reinterpret_cast<const f4*>(p.bias + col);
     if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
   }
-  float ymax = 0.f;                                   // running max|y| (p.y_amax)
+  FrameMax ymax;                                      // per-frame running max|y| (p.y_amax)
   auto offs = [&](int m, int64_t& yo, int64_t& ro) {
     if (p.ylin && p.rlin) {
       yo = (int64_t)m * p.ysw + col;
@@ -286,23 +285,29 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     int64_t yo[EB];
     f4 res[EB];
     bool ok[EB];
+    int fn[EB];                                       // frame of the row (max|y| slots, F16 scale)
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
       const int m = wrow0 + i * 16 + rr0 + RPP * e;
       ok[e] = cval && m < p.M;
       res[e] = f4{0.f, 0.f, 0.f, 0.f};
       yo[e] = 0;
+      fn[e] = 0;
       if (ok[e]) {
         int64_t ro;
         offs(m, yo[e], ro);
         if (p.res_mode != PRPE_RES_NONE) res[e] = *reinterpret_cast<const f4*>(p.r + ro);
+        if (F16 || p.y_amax) fn[e] = m / p.HoWo;
       }
     }
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
       f4 v = *reinterpret_cast<const f4*>(ct + (rr0 + RPP * e) * CS + cc * 4);
       if (!ok[e]) continue;
-      if constexpr (F16) v = v * inv_sa;   // exact (power of two)
+      if constexpr (F16) {                            // 2^(e - 15) of the row's frame: exact
+        const float am = DUAL ? fmaxf(p.x_amax[fn[e]], p.x2_amax[fn[e]]) : p.x_amax[fn[e]];
+        v = v * ldexpf(1.f, f16_scale_exp(am) - 15);
+      }
       v = v * sc4 + bi4;
       if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];
 #pragma unroll
@@ -318,10 +323,10 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       } else {
         *reinterpret_cast<f4*>(p.y + yo[e]) = v;
       }
-      ymax = fmaxf(ymax, amax4(v));
+      if (p.y_amax) ymax.add(p.y_amax, fn[e], amax4(v));
     }
   }
-  if (p.y_amax) amax_commit(p.y_amax, ymax);
+  if (p.y_amax) frame_amax_final(p.y_amax, ymax);
 }
 
 template <int NW, int TM, int TN, int NP, int STAGES, bool F16 = false>

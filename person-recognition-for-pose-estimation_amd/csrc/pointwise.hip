@@ -534,7 +534,10 @@ __global__ __launch_bounds__(256) void layernorm_reg_kernel(const float* __restr
 }
 
 // ------------------------------------------------------------------------- l2norm
-__global__ __launch_bounds__(256) void l2norm_kernel(const float* x, float* emb, float* norm, int rows, int C) {
+// emb = x / max(||x||, eps): eps = 0 is IR-50's torch.div(x, norm) (net_adaface.py:334-335),
+// eps = 1e-12 is F.normalize's clamp_min (face_recognition/module.py:137-138); norm = ||x||
+__global__ __launch_bounds__(256) void l2norm_kernel(const float* x, float* emb, float* norm, int rows, int C,
+                                                     float eps) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int lane = threadIdx.x & 63;
@@ -542,7 +545,8 @@ __global__ __launch_bounds__(256) void l2norm_kernel(const float* x, float* emb,
   double s = 0.0;
   for (int c = lane; c < C; c += 64) s += (double)xr[c] * xr[c];
   const float nrm = (float)sqrt(warp_sum_d(s));
-  for (int c = lane; c < C; c += 64) emb[(int64_t)row * C + c] = xr[c] / nrm;
+  const float den = fmaxf(nrm, eps);
+  for (int c = lane; c < C; c += 64) emb[(int64_t)row * C + c] = xr[c] / den;
   if (lane == 0) norm[row] = nrm;
 }
 
@@ -586,7 +590,7 @@ __global__ __launch_bounds__(256) void dfl_decode_kernel(DflK p) {
 // ------------------------------------------------------------------------- copy_pad
 // y[n,h,w,c] = c < x.c ? x[n,h,w,c] : 0  (layout change + channel zero-padding, e.g. NCHW
 // frames -> NHWC4 so the 7x7 stem takes the vectorised implicit-GEMM path)
-// (+ optional max|y| into *y_amax: the stem's precision-3 activation scale)
+// (+ optional per-frame max|y| into y_amax[n]: the stem's precision-3 activation scale)
 struct CopyK { prpe_view x, y; int per_row, chunks; float* y_amax; };
 // Y4: y is 4 contiguous, 16-B aligned channels per pixel (the stem's NHWC4 buffer): one
 // 16-B store per pixel instead of four 4-B ones
@@ -595,8 +599,9 @@ __global__ __launch_bounds__(256) void copy_pad_kernel(CopyK p) {
   int row, w;
   row_pos(p.chunks, row, w);
   float m = 0.f;
+  const int n = row / p.y.h;                          // block-uniform (one row per block)
   if (w < p.per_row) {
-    const int n = row / p.y.h, h = row - n * p.y.h;
+    const int h = row - n * p.y.h;
     float* y = p.y.ptr + voff(p.y, n, h, w, 0);
     if constexpr (Y4) {
       float v[4];
@@ -614,7 +619,7 @@ __global__ __launch_bounds__(256) void copy_pad_kernel(CopyK p) {
       }
     }
   }
-  if (p.y_amax) amax_commit(p.y_amax, m);
+  if (p.y_amax) amax_commit(p.y_amax + n, m);
 }
 
 inline unsigned nblocks(int64_t total, int bs = 256) { return (unsigned)((total + bs - 1) / bs); }
@@ -781,9 +786,11 @@ extern "C" int prpe_layernorm(const float* x, int64_t xs, float* y, int64_t ys, 
   return launch_status();
 }
 
-extern "C" int prpe_l2norm(const float* x, float* emb, float* norm, int32_t rows, int32_t C, void* stream) {
-  if (!x || !emb || !norm || rows <= 0 || C <= 0) return PRPE_EINVAL;
-  hipLaunchKernelGGL(l2norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), x, emb, norm, rows, C);
+extern "C" int prpe_l2norm(const float* x, float* emb, float* norm, int32_t rows, int32_t C, float eps,
+                           void* stream) {
+  if (!x || !emb || !norm || rows <= 0 || C <= 0 || !(eps >= 0.f)) return PRPE_EINVAL;
+  hipLaunchKernelGGL(l2norm_kernel, dim3((rows + 3) / 4), dim3(256), 0, as_stream(stream), x, emb, norm, rows, C,
+                     eps);
   return launch_status();
 }
 

@@ -11,7 +11,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libprpe.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 
 class PrpeError(RuntimeError):
@@ -60,7 +60,7 @@ SIGNATURES = {
     "prpe_attention": (C.c_int, [_P, _P, _I, _I, _I, _I, _F, _P]),
     "prpe_psa_attention": (C.c_int, [_VP, _VP, _VP, _I, _I, _I, _F, _P]),
     "prpe_dfl_decode": (C.c_int, [_P, _P, _I, _I, _I, C.POINTER(C.c_int32), C.POINTER(C.c_float), _P]),
-    "prpe_l2norm": (C.c_int, [_P, _P, _P, _I, _I, _P]),
+    "prpe_l2norm": (C.c_int, [_P, _P, _P, _I, _I, C.c_float, _P]),
     "prpe_nms_workspace_bytes": (C.c_int64, [_I, _I, _I, _I]),
     "prpe_nms": (C.c_int, [_P, _I, _I, _I, _I, _F, _F, _I, _I, _P, _P, _P, _L, _P]),
     "prpe_softargmax": (C.c_int, [_P, _I, _I, _I, _I, _P, _P, _P, _P, _P]),

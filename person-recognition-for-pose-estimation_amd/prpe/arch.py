@@ -10,7 +10,9 @@ Citations (reference = /root/reference):
   * ViTPose: ``CustomVitPose`` (modify_models.py:348-385) + transformers ViTPose-B (simple decoder)
 
 ``state_dict_spec()`` returns [(key, shape, kind)] for the 2130 entries; it is checked
-against the reference model's own ``state_dict()`` by tests/test_oracle_pinning.py.
+against the reference model's own ``state_dict()`` (keys and shapes recorded by
+oracle/make_golden_evalsteps.py into tests/golden/sd_keys_ref.json) by
+tests/test_abi_and_host.py::test_state_dict_spec_matches_reference_keys.
 """
 from __future__ import annotations
 

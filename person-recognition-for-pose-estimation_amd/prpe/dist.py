@@ -1,10 +1,13 @@
 """Multi-GPU frame sharding + the one exchange of the path.
 
 Frames are independent in eval mode (BN uses running statistics; the YOLO normalisation is
-per sample, modify_models.py:84-85), so a global batch shards contiguously over ranks with
-no collective on the data path. The exchange is the all-gather of each rank's padded
+per sample, modify_models.py:84-85; the precision-3 activation scales are per frame,
+engine.Engine.amax_slot), so a global batch shards contiguously over ranks with no
+collective on the data path. The exchange is the all-gather of each rank's padded
 detections [B_local, max_det, 6] + counts [B_local] (RCCL over xGMI with backend "nccl" on
 ROCm; gloo on CPU for tests), giving every rank the whole batch's detections in frame order.
+A ragged global batch (B_global % world != 0) is padded to the largest shard for the
+collective and trimmed afterwards.
 """
 from __future__ import annotations
 
@@ -19,19 +22,36 @@ def shard_range(global_batch: int, world: int, rank: int) -> tuple[int, int]:
     return start, start + base + (1 if rank < extra else 0)
 
 
-def gather_detections(dets: torch.Tensor, counts: torch.Tensor, group=None):
-    """All-gather equal-shaped per-rank (dets [b,D,6], counts [b]) -> ([W*b,D,6], [W*b])."""
+def gather_tensor(t: torch.Tensor, global_batch: int | None = None, group=None) -> torch.Tensor:
+    """All-gather the per-rank shard ``t`` [b_r, ...] along dim 0 -> [B_global, ...] in rank
+    (= frame) order. ``global_batch``: total frames when the shards may be ragged (the shard
+    of rank r is shard_range(global_batch, world, r)); None = equal shards."""
     world = dist.get_world_size(group)
     if world == 1:
-        return dets, counts
+        return t
+    if global_batch is None:
+        sizes = [t.shape[0]] * world
+    else:
+        sizes = [e - s for s, e in (shard_range(global_batch, world, r) for r in range(world))]
+        me = dist.get_rank(group)
+        if t.shape[0] != sizes[me]:
+            raise ValueError(f"rank {me} holds {t.shape[0]} frames, shard_range says {sizes[me]}")
+    cap = max(sizes)
+    t = t.contiguous()
+    if t.shape[0] < cap:                                  # pad the ragged shard
+        t = torch.cat([t, t.new_zeros((cap - t.shape[0],) + tuple(t.shape[1:]))], 0)
     if dist.get_backend(group) == "nccl":
-        gd = torch.empty((world * dets.shape[0],) + tuple(dets.shape[1:]), device=dets.device, dtype=dets.dtype)
-        gc = torch.empty((world * counts.shape[0],), device=counts.device, dtype=counts.dtype)
-        dist.all_gather_into_tensor(gd, dets.contiguous(), group=group)
-        dist.all_gather_into_tensor(gc, counts.contiguous(), group=group)
-        return gd, gc
-    ld = [torch.empty_like(dets) for _ in range(world)]
-    lc = [torch.empty_like(counts) for _ in range(world)]
-    dist.all_gather(ld, dets.contiguous(), group=group)
-    dist.all_gather(lc, counts.contiguous(), group=group)
-    return torch.cat(ld, 0), torch.cat(lc, 0)
+        g = torch.empty((world * cap,) + tuple(t.shape[1:]), device=t.device, dtype=t.dtype)
+        dist.all_gather_into_tensor(g, t, group=group)
+        parts = list(g.split(cap, 0))
+    else:
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=group)
+    if all(s == cap for s in sizes):
+        return torch.cat(parts, 0)
+    return torch.cat([p[:s] for p, s in zip(parts, sizes)], 0)
+
+
+def gather_detections(dets: torch.Tensor, counts: torch.Tensor, global_batch: int | None = None, group=None):
+    """All-gather per-rank (dets [b,D,6], counts [b]) -> ([B_global,D,6], [B_global])."""
+    return gather_tensor(dets, global_batch, group), gather_tensor(counts, global_batch, group)

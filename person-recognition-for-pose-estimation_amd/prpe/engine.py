@@ -38,7 +38,7 @@ BN_EPS = 1e-5
 # multiplies logit errors by the stride; the large adapters and the ViT run the bf16 3-term
 # split.
 AUTO_POLICY = {"trunk": 3, "yolo_adapter": 0, "yolo_net": 2, "adaface": 0, "vit": 0}
-AMAX_SLOTS = 4096
+AMAX_TENSORS = 128                  # max|y| slot arrays per forward (one [B] array per conv output)
 # PRPE_PLANES=0 keeps every activation in fp32 (A/B runs of the planes-format handoff)
 PLANES_ON = os.environ.get("PRPE_PLANES", "1") != "0"
 # 3x3/1 convs with Co <= 4 (the last conv of the YOLO and ViTPose adapters) as the tap rewrite
@@ -76,8 +76,9 @@ class Engine:
         self._aux: dict[str, torch.Tensor] = {}
         self.watch: set[str] = set()      # pack names whose launches get HIP-event timing
         self.events: dict[str, list] = {}
-        self._amax_pool = None             # device max|y| slots of conv outputs (precision 3)
+        self._amax_pool = None             # device per-frame max|y| slots of conv outputs (precision 3)
         self._amax_i = 0
+        self._amax_b = 1
 
     def prec(self, comp):
         return _Prec(self, comp)
@@ -113,20 +114,23 @@ class Engine:
             self._packs[name] = p
         return p
 
-    # ---- max|y| tracking: every conv output gets a device slot its epilogue raises to max|y|;
-    # a precision-3 consumer reads it to pick its activation scale. Slots are zeroed once per
-    # forward (amax_reset, at the start of the trunk).
-    def amax_reset(self):
-        if self._amax_pool is None:
-            self._amax_pool = torch.zeros(AMAX_SLOTS, device=self.device, dtype=torch.float32)
+    # ---- max|y| tracking: every precision-3 conv output gets a [B] array of per-FRAME device
+    # slots its epilogue raises to max|y[n]|; a precision-3 consumer reads slot n to pick frame
+    # n's activation scale, so a frame's arithmetic never depends on its batch-mates (or on the
+    # shard it lands in). The pool is zeroed once per forward (amax_reset, start of the trunk).
+    def amax_reset(self, batch: int):
+        n = AMAX_TENSORS * batch
+        if self._amax_pool is None or self._amax_pool.numel() < n:
+            self._amax_pool = torch.zeros(n, device=self.device, dtype=torch.float32)
         else:
             self._amax_pool.zero_()
         self._amax_i = 0
+        self._amax_b = batch
 
-    def amax_slot(self):
-        if self._amax_pool is None or self._amax_i >= AMAX_SLOTS:
-            self.amax_reset()
-        t = self._amax_pool[self._amax_i:self._amax_i + 1]
+    def amax_slot(self, batch: int):
+        if self._amax_pool is None or batch != self._amax_b or self._amax_i >= AMAX_TENSORS:
+            raise RuntimeError("max|y| slot pool not reset for this batch (Engine.amax_reset)")
+        t = self._amax_pool[self._amax_i * batch:(self._amax_i + 1) * batch]
         self._amax_i += 1
         return t
 
@@ -166,7 +170,7 @@ class Engine:
         if prec == 3 and (not self._f16_ok(x, p, out) or (x2 is not None and x2_amax is None)):
             prec = 2
         xa = getattr(x, "_prpe_amax", None) if prec == 3 else None
-        ya = self.amax_slot() if self.precision == 3 else None
+        ya = self.amax_slot(B) if self.precision == 3 else None
         x_planes = getattr(x, "_prpe_planes", False)
         if x_planes and prec != 0:
             raise RuntimeError(f"{p.name}: planes-format input needs precision 0, got {prec}")
@@ -231,7 +235,7 @@ class Engine:
     def trunk(self, x_nchw, flip_w=False):
         """MultiTaskResNetFeatureExtractor (modify_models.py:427-437), torchvision v1.5.
         ``flip_w``: run on the W-mirrored frames (torch.flip(images, dims=[-1]))."""
-        self.amax_reset()
+        self.amax_reset(x_nchw.shape[0])
         with self.prec("trunk"):
             return self._trunk(x_nchw, flip_w)
 
@@ -253,7 +257,7 @@ class Engine:
                 del self._aux[k]                       # one batch shape at a time
             buf = torch.zeros(B0, H0 + 6, W0 + 8, 4, device=self.device, dtype=torch.float32)
             self._aux[key] = buf
-        amax = self.amax_slot()
+        amax = self.amax_slot(B0)
         ops.copy_pad(ops.nhwc(x_nchw), buf[:, 3:3 + H0, 3:3 + W0, :], flip_w=flip_w, y_amax=amax)
         v = buf.as_strided((B0, H0 + 6, W0, 32), (buf.stride(0), buf.stride(1), 4, 1))
         v._prpe_amax = amax

@@ -28,6 +28,7 @@ import torch
 from . import ops
 from .pack import pack_matrix
 
+F_NORMALIZE_EPS = 1e-12          # torch.nn.functional.normalize default eps
 COCO_FLIP_PAIRS = [(1, 2), (3, 4), (5, 6), (7, 8), (9, 10), (11, 12), (13, 14), (15, 16)]  # datamodule.py:25-34
 
 
@@ -67,7 +68,7 @@ class FaceRecognitionEval:
         k = kernel.to(self.model.device, torch.float32).contiguous()
         d, ncls = k.shape
         kn = torch.empty_like(k)
-        ops.l2norm(k, kn, torch.empty(d, device=k.device))            # F.normalize(kernel), dim=1
+        ops.l2norm(k, kn, torch.empty(d, device=k.device), F_NORMALIZE_EPS)   # F.normalize(kernel), dim=1
         self.classes = ncls
         self.pack = pack_matrix("ada_face.head:logits", kn.t().cpu(), 1, 1, d, 1, 0, self.model.device,
                                 scale=torch.full((ncls,), self.s))
@@ -76,7 +77,7 @@ class FaceRecognitionEval:
         B, d = embeddings.shape
         e = embeddings.contiguous().float()
         en = torch.empty_like(e)
-        ops.l2norm(e, en, torch.empty(B, device=e.device))            # F.normalize(embeddings)
+        ops.l2norm(e, en, torch.empty(B, device=e.device), F_NORMALIZE_EPS)   # F.normalize(embeddings)
         out = torch.empty(B, 1, 1, self.classes, device=e.device)
         ops.conv2d(en.view(B, 1, 1, d), self.pack, out, precision=self.precision)
         return out.view(B, self.classes)

@@ -8,20 +8,25 @@ Same surface the eval steps touch:
   * ``state_dict()/load_state_dict()`` with the reference's 2130 keys;
   * ``model.yolo_face.yolo.head.stride`` / ``yolo_person...`` (a fresh ``Head`` after
     ``modify_yolo`` has stride zeros, nn.py:238 -> eval boxes are 0; honoured as given);
-  * ``model.ada_face.head.kernel`` for the face-recognition eval logits.
+  * ``model.ada_face.head.kernel`` for the face-recognition eval logits;
+  * the branches as ``nn.Module`` trees with the reference's parameter names
+    (``model.vit_pose.adapter.parameters()``, ``model.yolo_face.parameters()`` ..., prpe.modules)
+    and ``model.vit_pose.vit_pose(pixel_values)`` -> ``.heatmaps`` (BASELINE config 3).
 Plus ``forward_all(x)``: trunk once, then face-YOLO + AdaFace + ViTPose (BASELINE config 4).
 
 Eval-only: the reference's training outputs/backward are out of scope.
 """
 from __future__ import annotations
 
+import itertools
 from dataclasses import dataclass
 from types import SimpleNamespace
 
 import torch
 
-from . import arch
+from . import arch, ops
 from .engine import Engine
+from .modules import branch_trees
 
 
 @dataclass
@@ -43,6 +48,7 @@ class CombinedModel:
         self.yolo_face = SimpleNamespace(yolo=SimpleNamespace(head=SimpleNamespace(stride=torch.zeros(3))))
         self.yolo_person = SimpleNamespace(yolo=SimpleNamespace(head=SimpleNamespace(stride=torch.zeros(3))))
         self.ada_face = SimpleNamespace(head=SimpleNamespace(kernel=None))
+        self.vit_pose = None
         self.engine = None
         if state_dict is not None:
             self.load_state_dict(state_dict)
@@ -54,9 +60,13 @@ class CombinedModel:
         unexpected = [k for k in state_dict if k not in keys]
         if strict and (missing or unexpected):
             raise KeyError(f"state_dict mismatch: missing={missing[:5]} unexpected={unexpected[:5]}")
+        strides = {b: getattr(self, b).yolo.head.stride for b in ("yolo_face", "yolo_person")}
         self._sd = {k: v.detach().cpu() for k, v in state_dict.items()}
-        if "ada_face.head.kernel" in self._sd:
-            self.ada_face.head.kernel = self._sd["ada_face.head.kernel"].to(self.device)
+        trees = branch_trees(self._sd, self)
+        for b, t in trees.items():
+            setattr(self, b, t)
+        for b, st in strides.items():          # a reload keeps the stride the caller set
+            getattr(self, b).yolo.head.stride = st
         self.engine = Engine(self._sd, self.device, self.precision)
         return SimpleNamespace(missing_keys=missing, unexpected_keys=unexpected)
 
@@ -75,6 +85,13 @@ class CombinedModel:
 
     def float(self):
         return self
+
+    # parameters of the branches (the trunk's are in the state_dict under ``backbone.``)
+    def parameters(self, recurse: bool = True):
+        trunk = (torch.nn.Parameter(v) for k, v in self._sd.items()
+                 if k.startswith("backbone.") and torch.is_floating_point(v) and "running_" not in k)
+        return itertools.chain(trunk, *(getattr(self, b).parameters() for b in
+                                        ("yolo_face", "yolo_person", "ada_face", "vit_pose")))
 
     def eval(self):
         self.training = False
@@ -112,6 +129,19 @@ class CombinedModel:
         return e.adaface(feat)
 
     __call__ = forward
+
+    @torch.no_grad()
+    def vitpose_from_pixels(self, pixel_values):
+        """``VitPoseForPoseEstimation(pixel_values)`` (site-packages modeling_vitpose.py:190-278),
+        as the reference calls it at modify_models.py:383-385: pixel_values [B,3,256,192] ->
+        PoseOutput(heatmaps [B,17,64,48]). BASELINE config 3."""
+        x = pixel_values
+        if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
+                and tuple(x.shape[1:]) == (3,) + tuple(arch.VIT_IMG)):
+            raise ValueError(f"expected float32 CUDA(HIP) pixel_values [B,3,{arch.VIT_IMG[0]},{arch.VIT_IMG[1]}]")
+        e = self.engine
+        with e.prec("vit"):
+            return PoseOutput(heatmaps=e.vit_backbone(ops.nhwc(x)))
 
     @torch.no_grad()
     def forward_all(self, x, face_stride=None, concurrent=True):

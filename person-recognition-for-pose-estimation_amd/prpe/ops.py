@@ -40,10 +40,14 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
            y_amax=None, x2=None, x2_amax=None, x_planes=False, y_planes=False):
     """y = EPI(conv(PRO(x))) with a ``ConvPack`` (see prpe.pack).
 
-    precision 3 (split fp16) needs ``x_amax``: a 1-element device tensor bounding max|x| (e.g.
-    the ``y_amax`` its producer raised). ``y_amax`` (any precision): 1-element device tensor the
-    kernel raises to max|y| (zero it first)."""
+    precision 3 (split fp16) needs ``x_amax``: a [N] device tensor, x_amax[n] bounding max|x[n]|
+    per frame (e.g. the ``y_amax`` its producer raised). ``y_amax`` (any precision): [N] device
+    tensor the kernel raises to max|y[n]| per frame (zero it first)."""
     d = ConvDesc()
+    N = x.shape[0]
+    for a in (x_amax, y_amax, x2_amax):
+        if a is not None and (a.dtype != torch.float32 or not a.is_cuda or a.numel() < N or not a.is_contiguous()):
+            raise ValueError(f"prpe_conv2d[{pack.name}]: max|x| slots must be a contiguous float32 device [N]")
     if precision == 3:
         h16, l16, s16 = pack.f16_planes()
         d.w_h16, d.w_l16, d.scale16 = h16.data_ptr(), l16.data_ptr(), s16.data_ptr()
@@ -96,8 +100,8 @@ def maxpool(x, y, k, stride, pad):
 
 def copy_pad(x, y, flip_w=False, y_amax=None):
     """y = x zero-padded in C; ``flip_w`` reads x mirrored along W (a negative-stride view,
-    so the flip-test pass needs no flipped copy of the frames); ``y_amax`` (1-element device
-    tensor, zeroed) is raised to max|y|."""
+    so the flip-test pass needs no flipped copy of the frames); ``y_amax`` ([N] device tensor,
+    zeroed) is raised to max|y[n]| per frame."""
     xv = view(x)
     if flip_w:
         xv.ptr = x.data_ptr() + (x.shape[2] - 1) * x.stride(2) * x.element_size()
@@ -144,9 +148,12 @@ def dfl_decode(head, out, nc, level_hw, strides):
     return out
 
 
-def l2norm(x, emb, norm):
+def l2norm(x, emb, norm, eps=0.0):
+    """emb = x / max(||x||, eps) per row, norm = ||x||. eps 0: torch.div(x, norm) (IR-50 output);
+    eps 1e-12: F.normalize."""
     rows, c = x.shape
-    check(lib().prpe_l2norm(x.data_ptr(), emb.data_ptr(), norm.data_ptr(), rows, c, _stream()), "prpe_l2norm")
+    check(lib().prpe_l2norm(x.data_ptr(), emb.data_ptr(), norm.data_ptr(), rows, c, float(eps), _stream()),
+          "prpe_l2norm")
     return emb, norm
 
 
@@ -160,8 +167,13 @@ def nms(pred, layout, conf=0.001, iou=0.65, max_nms=30000, max_det=300):
         N, nc = pred.shape[1], pred.shape[2] - 4
     out = torch.empty(B, max_det, 6, device=pred.device, dtype=torch.float32)
     cnt = torch.empty(B, device=pred.device, dtype=torch.int32)
+    # N*nc above the kernel's LDS key capacity: keys + segmented sort in a global workspace
+    nbytes = lib().prpe_nms_workspace_bytes(B, N, nc, max_nms)
+    if nbytes < 0:
+        raise RuntimeError("prpe_nms_workspace_bytes failed")
+    ws = torch.empty((nbytes + 7) // 8, device=pred.device, dtype=torch.int64) if nbytes else None
     check(lib().prpe_nms(pred.data_ptr(), B, N, nc, layout, conf, iou, max_nms, max_det, out.data_ptr(),
-                         cnt.data_ptr(), None, 0, _stream()), "prpe_nms")
+                         cnt.data_ptr(), _ptr(ws), nbytes, _stream()), "prpe_nms")
     return out, cnt
 
 

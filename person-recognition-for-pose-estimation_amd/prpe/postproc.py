@@ -27,7 +27,7 @@ def non_max_suppression(outputs: torch.Tensor, confidence_threshold=0.001, iou_t
     out, cnt = non_max_suppression_padded(outputs, confidence_threshold, iou_threshold)
     counts = cnt.tolist()
     if any(c < 0 for c in counts):
-        raise RuntimeError("prpe_nms: more candidates per image than the kernel's LDS capacity")
+        raise RuntimeError("prpe_nms: candidate overflow")
     return [out[i, :c] for i, c in enumerate(counts)]
 
 

@@ -1,4 +1,7 @@
-"""Worker of tests/test_dist_gloo.py (one process per rank, gloo, 127.0.0.1)."""
+"""Worker of tests/test_dist_gloo.py (one process per rank, gloo, 127.0.0.1).
+
+    python _dist_worker.py OUT [GLOBAL_BATCH]     (rendezvous from the environment)
+"""
 import os
 import sys
 
@@ -12,16 +15,19 @@ from prpe.dist import gather_detections, shard_range  # noqa: E402
 
 def main():
     rank, world, out = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"]), sys.argv[1]
+    gb = int(sys.argv[2]) if len(sys.argv) > 2 else 6
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        s, e = shard_range(6, world, rank)
+        s, e = shard_range(gb, world, rank)
         dets = torch.zeros(e - s, 300, 6)
         cnt = torch.zeros(e - s, dtype=torch.int32)
         for i, f in enumerate(range(s, e)):   # frame f has (f % 3) boxes valued f
             cnt[i] = f % 3
             dets[i, :f % 3] = float(f)
-        gd, gc = gather_detections(dets, cnt)
-        torch.save({"gd": gd, "gc": gc}, f"{out}.{rank}")
+        ragged = gb % world != 0
+        gd, gc = gather_detections(dets, cnt, global_batch=gb if ragged else None)
+        torch.save({"gd": gd, "gc": gc, "rank": rank, "world": world,
+                    "local_rank": int(os.environ.get("LOCAL_RANK", "-1"))}, f"{out}.{rank}")
     finally:
         dist.destroy_process_group()
 

@@ -159,3 +159,44 @@ def test_synth_is_deterministic():
     c = synth.uniform(4, "x", (1000,))
     assert torch.equal(a, b) and not torch.equal(a, c)
     assert float(a.min()) >= 0.0 and float(a.max()) < 1.0
+
+
+def test_branch_module_surface_for_configure_optimizers(state_dict):
+    """The callers' configure_optimizers reach into the branches: the trees
+    carry the reference's parameter names and storage, buffers stay buffers, the YOLO head
+    stride is a plain attribute (never in state_dict), and an optimizer can be built."""
+    m = CombinedModel(state_dict, device="cuda")      # packs lazily: no GPU touched here
+    names = dict(m.vit_pose.adapter.named_parameters())
+    assert set(names) == {k[len("vit_pose.adapter."):] for k in state_dict
+                          if k.startswith("vit_pose.adapter.") and "running_" not in k and "num_batches" not in k}
+    assert names["0.weight"].data_ptr() == state_dict["vit_pose.adapter.0.weight"].data_ptr()
+    vp = dict(m.vit_pose.vit_pose.named_parameters())
+    assert "backbone.encoder.layer.11.mlp.fc2.weight" in vp and "head.conv.weight" in vp
+    yb = dict(m.yolo_face.named_buffers())
+    assert "adapter.1.running_mean" in yb and "adapter.1.running_mean" not in dict(m.yolo_face.named_parameters())
+    assert "yolo.head.stride" not in m.yolo_face.state_dict()
+    assert torch.equal(m.yolo_face.yolo.head.stride, torch.zeros(3))
+    m.yolo_face.yolo.head.stride = torch.tensor([8.0, 16.0, 32.0])
+    m.load_state_dict(state_dict)                      # a reload keeps the caller's stride
+    assert m.yolo_face.yolo.head.stride.tolist() == [8.0, 16.0, 32.0]
+    ada = list(m.ada_face.adapter.parameters()) + list(m.ada_face.parameters())   # module.py:179-180
+    import warnings
+    with warnings.catch_warnings():       # the reference's list repeats the adapter's parameters too
+        warnings.simplefilter("ignore", UserWarning)
+        opt = torch.optim.Adam(ada + list(m.yolo_person.parameters()), lr=1e-3)
+    assert len(opt.param_groups[0]["params"]) == len(ada) + len(list(m.yolo_person.parameters()))
+    n_ref = sum(1 for k, v in state_dict.items() if "running_" not in k and "num_batches" not in k
+                and k.split(".")[-1] not in ("t", "batch_mean", "batch_std"))
+    assert sum(1 for _ in m.parameters()) == n_ref
+    assert m.ada_face.head.kernel is None              # the synthetic state_dict has no head kernel
+    with pytest.raises(ValueError):
+        m.vit_pose.vit_pose(torch.zeros(1, 3, 256, 192))   # CPU tensor: the HIP path only
+
+
+def test_state_dict_spec_matches_reference_keys():
+    """arch.state_dict_spec() == the reference CombinedModel's own state_dict() (keys and
+    shapes, recorded by oracle/make_golden_evalsteps.py into tests/golden/sd_keys_ref.json)."""
+    import json
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "sd_keys_ref.json")))
+    spec = {k: list(s) for k, s, _ in arch.state_dict_spec()}
+    assert spec == {k: list(s) for k, s in ref.items()}

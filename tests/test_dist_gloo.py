@@ -1,15 +1,18 @@
-"""CPU: the N > 1 path (frame sharding + all-gather of padded detections) with world_size 2
-over gloo, exactly the logic bench.py runs over RCCL."""
+"""CPU: the N > 1 path (frame sharding + all-gather of padded detections) over gloo, exactly
+the logic bench.py runs over RCCL, at world sizes 2 and 4 (even and ragged global batches),
+and bench.py's own launcher (one child per rank, rendezvous env on 127.0.0.1)."""
 import os
 import socket
 import subprocess
 import sys
 
+import pytest
 import torch
 
 from prpe.dist import shard_range
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 
 
 def _free_port():
@@ -29,19 +32,42 @@ def test_shard_range_covers_batch_exactly():
             assert max(e - s for s, e in r) - min(e - s for s, e in r) <= 1
 
 
-def test_gather_detections_world2_gloo(tmp_path):
+def _check(out, world, gb):
+    for r in range(world):
+        res = torch.load(f"{out}.{r}", weights_only=True)
+        gd, gc = res["gd"], res["gc"]
+        assert res["rank"] == r and res["world"] == world
+        assert gd.shape == (gb, 300, 6) and gc.tolist() == [f % 3 for f in range(gb)]
+        for f in range(gb):
+            assert torch.all(gd[f, :f % 3] == f) and torch.all(gd[f, f % 3:] == 0)
+
+
+@pytest.mark.parametrize("world,gb", [(2, 6), (4, 7)])
+def test_gather_detections_gloo(tmp_path, world, gb):
     port = _free_port()
     out = str(tmp_path / "res")
     procs = []
-    for r in range(2):
-        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
                    CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_worker.py"), out], env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_worker.py"), out, str(gb)], env=env))
     for p in procs:
         assert p.wait(timeout=180) == 0
-    for r in range(2):
-        res = torch.load(f"{out}.{r}", weights_only=True)
-        gd, gc = res["gd"], res["gc"]
-        assert gd.shape == (6, 300, 6) and gc.tolist() == [f % 3 for f in range(6)]
-        for f in range(6):
-            assert torch.all(gd[f, :f % 3] == f) and torch.all(gd[f, f % 3:] == 0)
+    _check(out, world, gb)
+
+
+def test_bench_launcher_spawns_ranks(tmp_path, monkeypatch):
+    """bench.py --gpus N without WORLD_SIZE: launch_children starts N processes with the
+    rendezvous environment (here a gloo worker instead of bench.py itself: no GPU)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setenv("CUDA_VISIBLE_DEVICES", "")
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "")
+    out = str(tmp_path / "res")
+    rc = bench.launch_children(3, [sys.executable, os.path.join(HERE, "_dist_worker.py"), out, "5"])
+    assert rc == 0
+    _check(out, 3, 5)
+    for r in range(3):
+        assert torch.load(f"{out}.{r}", weights_only=True)["local_rank"] == r
+    # a failing rank makes the launcher fail
+    assert bench.launch_children(2, [sys.executable, "-c", "import os,sys; sys.exit(int(os.environ['RANK']) + 3)"]) != 0

@@ -1,8 +1,10 @@
-"""GPU: the eval-step kernels around the model against the oracle's
-restatement of the reference code (oracle/model_ref.py: pose_flip_average restates
-pose_estimation/module.py:476-484, face_recognition_eval restates face_recognition/module.py:
-137-145). The reference runs these lines inline in Lightning validation steps, so no golden
-vectors exist for them: parity is pinned to the restatement.
+"""GPU: the eval-step kernels around the model against the
+REFERENCE's own validation steps (tests/golden/golden_flip.npz, golden_facerec.npz:
+oracle/make_golden_evalsteps.py executed PoseEstimationModule.validation_step, module.py:
+451-570, and FaceRecognitionModule.validation_step, face_recognition/module.py:119-157, in the
+build container with stub models; inputs rebuilt by oracle/fixtures.py) and against the
+oracle's restatements (oracle/model_ref.py pose_flip_average / face_recognition_eval, which the
+generator checked bit-exact against those runs).
 
 Tolerances: flip average bit-exact on the same heatmaps (same (a + b) * 0.5 in fp32); the
 end-to-end flip test within the heatmap bar (1e-3 abs); cross-entropy within 1e-5 relative
@@ -12,7 +14,12 @@ of a row are closer than 1e-4 (fp32 GEMM rounding can swap a near-tie).
 import pytest
 import torch
 
+import os
+
+import numpy as np
+
 from oracle import model_ref as R
+from oracle.fixtures import facerec_inputs, flip_inputs
 from prpe import CombinedModel, ops, synth
 from prpe.evalsteps import FaceRecognitionEval, flip_partner, pose_flip_test
 
@@ -27,6 +34,37 @@ def test_flip_average_bit_exact(mode):
     got = ops.flip_average(heat.cuda(), heat_f.cuda(), flip_partner(17), 0 if mode == "reference" else 1)
     ref = R.pose_flip_average(heat, heat_f.clone(), mode)
     assert torch.equal(got.cpu(), ref)
+
+
+def _golden(name):
+    with np.load(os.path.join(os.path.dirname(__file__), "golden", name), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def test_flip_average_vs_reference_validation_step():
+    """prpe_flip_average (mode 0) == the averaged heatmaps the reference's flip block handed to
+    _get_keypoints_from_heatmaps, bit for bit; prpe_softargmax on them == its coords/scores."""
+    g = _golden("golden_flip.npz")
+    heat, heat_f = flip_inputs()
+    assert heat.double().sum().item() == g["heat_sum"] and heat_f.double().sum().item() == g["heat_flipped_sum"]
+    got = ops.flip_average(heat.cuda(), heat_f.cuda(), flip_partner(17), 0)
+    assert np.array_equal(got.cpu().numpy(), g["avg"])
+    c, s = ops.softargmax(got, boxes=torch.from_numpy(g["boxes"]).cuda())
+    np.testing.assert_allclose(c.cpu().numpy(), g["coords"], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(s.cpu().numpy(), g["scores"], rtol=1e-6, atol=1e-7)
+
+
+def test_face_recognition_eval_vs_reference_validation_step(model):
+    """FaceRecognitionEval on the reference validation step's inputs: val_loss / val_acc."""
+    g = _golden("golden_facerec.npz")
+    emb, kernel, labels = facerec_inputs()
+    assert emb.double().sum().item() == g["emb_sum"] and kernel.double().sum().item() == g["kernel_sum"]
+    model.ada_face.head.kernel = kernel.cuda()
+    fr = FaceRecognitionEval(model, s=64.0)
+    loss, acc, amax = fr(embeddings=emb.cuda(), labels=labels.cuda())
+    assert abs(loss.item() - float(g["val_loss"])) <= 1e-5 * max(1.0, abs(float(g["val_loss"])))
+    assert acc.item() == float(g["val_acc"])
+    assert np.array_equal(amax.cpu().numpy().astype(np.int64), g["argmax"])
 
 
 def test_flip_average_rejects_bad_args():

@@ -3,9 +3,10 @@ the same seeded frames/weights (bs=2, 640x640) and against the oracle.
 
 Tolerances (north_star): heatmaps and face embeddings within 1e-3 abs of the fp32 CPU
 reference; norms within 1e-3 relative; detection tensor within 1e-3 abs on cls scores
-and 5e-3 x max|box| on pixel box coordinates (stride-8..32 scaled); keypoint
-OKS delta <= 1e-3; NMS on our own det output is bit-exact vs the oracle NMS of the same
-tensor, and the end-to-end match rate vs the reference's NMS is reported.
+and 2e-3 x max|box| on pixel box coordinates (stride-8..32 scaled; measured 1.4 px on
+~930 px); keypoint OKS delta <= 1e-3; NMS on our own det output is bit-exact
+vs the oracle NMS of the same tensor, and the end-to-end detection match vs the reference's
+NMS on the reference's det tensor is 1.0 (measured; tests/test_gpu_batch.py covers bs=64/256).
 """
 import numpy as np
 import pytest
@@ -53,9 +54,9 @@ def test_face_detection_with_strides(model, frames, golden_model):
     ref = golden_model["det_face_s8"]
     np.testing.assert_allclose(det[:, 4], ref[:, 4], rtol=0, atol=1e-3)
     # pixel boxes (DFL expectation x stride 8..32) amplify logit rounding: an all-fp32-faithful
-    # run (precision=2 everywhere) differs by 0.48 px, "auto" by ~1.5 px, all 3-term by 3.9 px
-    # on ~750-930 px coordinates (tools/precision_sweep.py); tolerance 5e-3 x max coordinate
-    np.testing.assert_allclose(det[:, :4], ref[:, :4], rtol=0, atol=5e-3 * np.abs(ref[:, :4]).max())
+    # run (precision=2 everywhere) differs by 0.48 px, "auto" by ~1.5 px on ~750-930 px
+    # coordinates (tools/precision_sweep.py); tolerance 2e-3 x max coordinate
+    np.testing.assert_allclose(det[:, :4], ref[:, :4], rtol=0, atol=2e-3 * np.abs(ref[:, :4]).max())
 
 
 def test_pose_heatmaps_and_keypoints(model, frames, golden_model):
@@ -108,7 +109,7 @@ def test_nms_on_model_output_bit_exact_vs_oracle(model, frames, golden_model):
     ref = R.non_max_suppression(torch.from_numpy(golden_model["det_face_s8"]))
     rates = [nms_match_rate(a.cpu(), b) for a, b in zip(ours, ref)]
     print("end-to-end NMS detection match rate vs reference:", rates)
-    assert min(rates) >= 0.9
+    assert min(rates) == 1.0
 
 
 def _iou(a, b):

@@ -336,20 +336,27 @@ def test_conv_wave_kernel_prologue_residual_prelu(mode, tile):
 
 
 def _conv_p3(x, w, s, p, tile=0, amax=None, **kw):
-    """precision 3 (split fp16, scaled): x_amax = max|x| (or the given bound)."""
+    """precision 3 (split fp16, scaled): x_amax[n] = max|x[n]| per frame (or the given bound for
+    every frame); returns (y, max over frames of y_amax) after checking y_amax[n] == max|y[n]|."""
     pk = pack.pack_conv("t", w, s, p, DEV, scale=kw.pop("scale", None), bias=kw.pop("bias", None),
                         act=kw.pop("act", "none"), k_order=1 if w.shape[2] * w.shape[3] > 1 else 0)
     xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
     B, _, H, W = x.shape
     Ho, Wo = (H + 2 * p - w.shape[2]) // s + 1, (W + 2 * p - w.shape[3]) // s + 1
     y = torch.empty(B, Ho, Wo, w.shape[0], device=DEV)
-    xa = torch.tensor([float(x.abs().max()) if amax is None else amax], device=DEV)
-    ya = torch.zeros(1, device=DEV)
+    xa = (frame_amax(x) if amax is None else torch.full((B,), float(amax))).to(DEV)
+    ya = torch.zeros(B, device=DEV)
     r = kw.pop("res", None)
     rd = r.permute(0, 2, 3, 1).contiguous().to(DEV) if r is not None else None
     ops.conv2d(xd, pk, y, res=rd, precision=3, tile=tile, x_amax=xa, y_amax=ya, **kw)
     torch.cuda.synchronize()
-    return y.permute(0, 3, 1, 2).cpu(), float(ya.item())
+    assert torch.equal(ya.cpu(), frame_amax(y))
+    return y.permute(0, 3, 1, 2).cpu(), float(ya.max().item())
+
+
+def frame_amax(t):
+    """per-frame max|t| (the engine's y_amax slots), float32 CPU [B]"""
+    return t.detach().abs().flatten(1).amax(1).float().cpu()
 
 
 @pytest.mark.parametrize("tile", [0, 21, 22, 23, 24, 25, 26])
@@ -402,15 +409,15 @@ def test_conv_f16_split_residual_and_chained_amax():
     p1 = pack.pack_conv("a", w1, 1, 0, DEV, act="relu")
     p2 = pack.pack_conv("b", w2, 1, 1, DEV, act="relu", k_order=1)
     xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
-    xa = torch.tensor([float(x.abs().max())], device=DEV)
-    a1, a2 = torch.zeros(1, device=DEV), torch.zeros(1, device=DEV)
+    xa = frame_amax(x).to(DEV)
+    a1, a2 = torch.zeros(2, device=DEV), torch.zeros(2, device=DEV)
     t = torch.empty(2, 10, 10, 128, device=DEV)
     ops.conv2d(xd, p1, t, precision=3, x_amax=xa, y_amax=a1)
     y = torch.empty(2, 10, 10, 64, device=DEV)
     ops.conv2d(t, p2, y, res=r.permute(0, 2, 3, 1).contiguous().to(DEV), res_mode=RES_PRE, precision=3,
                x_amax=a1, y_amax=a2)
     torch.cuda.synchronize()
-    assert a1.item() == t.abs().max().item() and a2.item() == y.abs().max().item()
+    assert torch.equal(a1.cpu(), frame_amax(t)) and torch.equal(a2.cpu(), frame_amax(y))
     ref = ref_conv(ref_conv(x, w1, 1, 0, act="relu"), w2, 1, 1, act="relu", res=r, res_mode=RES_PRE)
     torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=2e-6)
 
@@ -434,7 +441,7 @@ def test_conv_dual_input_bottleneck_projection(precision, stride, cin, c2, co):
     xd = xb.permute(0, 2, 3, 1).contiguous().to(DEV)
     x2 = xd[:, ::stride, ::stride, :]
     y = torch.empty(B, Ho, Wo, co, device=DEV)
-    amax = lambda t: torch.tensor([float(t.abs().max())], device=DEV)
+    amax = lambda t: frame_amax(t).to(DEV)
     ops.conv2d(od, pk, y, precision=precision, x2=x2, x_amax=amax(o), x2_amax=amax(xb))
     torch.cuda.synchronize()
     ref = torch.relu(ref_conv(o, w3, 1, 0, scale=s3, bias=b3).double() +
@@ -528,10 +535,10 @@ def test_conv_y_amax_every_kernel_family():
         pk = pack.pack_conv("t", w, 1, k // 2, DEV, k_order=1 if k > 1 else 0)
         xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
         y = torch.empty(2, 9, 13, co, device=DEV)
-        ya = torch.zeros(1, device=DEV)
+        ya = torch.zeros(2, device=DEV)
         ops.conv2d(xd, pk, y, precision=2, tile=tile, y_amax=ya)
         torch.cuda.synchronize()
-        assert ya.item() == y.abs().max().item(), (co, tile)
+        assert torch.equal(ya.cpu(), frame_amax(y)), (co, tile)
 
 
 def test_conv_fp32_faithful_stem_scalar_path():
@@ -771,6 +778,27 @@ def test_l2norm():
     torch.testing.assert_close(emb.cpu(), x / n, rtol=0, atol=1e-7)
 
 
+def test_l2norm_zero_rows_eps():
+    """eps = 1e-12 is F.normalize (a zero row stays 0, face-rec eval); eps = 0 is the IR-50
+    output's torch.div(x, norm) (a zero row gives NaN there too)."""
+    x = rnd(8, 512, seed=46)
+    x[3] = 0.0
+    x[5] *= 1e-20                               # norm below eps: x / 1e-12
+    xd = x.to(DEV)
+    emb, nrm = torch.empty(8, 512, device=DEV), torch.empty(8, 1, device=DEV)
+    ops.l2norm(xd, emb, nrm, 1e-12)
+    torch.cuda.synchronize()
+    ref = torch.nn.functional.normalize(x)
+    torch.testing.assert_close(emb.cpu(), ref, rtol=1e-6, atol=1e-7)
+    assert torch.equal(emb[3].cpu(), torch.zeros(512)) and nrm[3].item() == 0.0
+    ops.l2norm(xd, emb, nrm, 0.0)
+    torch.cuda.synchronize()
+    ref0 = torch.div(x, torch.norm(x, 2, 1, True))
+    assert torch.isnan(emb[3]).all() and torch.isnan(ref0[3]).all()
+    ok = torch.arange(8) != 3
+    torch.testing.assert_close(emb.cpu()[ok], ref0[ok], rtol=1e-6, atol=1e-7)
+
+
 @pytest.mark.parametrize("stride", [(0.0, 0.0, 0.0), (8.0, 16.0, 32.0)])
 def test_dfl_decode_matches_oracle_head(stride):
     from oracle.model_ref import make_anchors
@@ -800,13 +828,13 @@ def test_copy_pad_nchw_to_padded_nhwc(yc, flip):
     x = torch.randn(2, 3, 13, 21)
     buf = torch.full((2, 13 + 6, 21 + 8, yc), 7.0, device=DEV)
     y = buf[:, 3:3 + 13, 4:4 + 21, :]
-    ya = torch.zeros(1, device=DEV)
+    ya = torch.zeros(2, device=DEV)
     ops.copy_pad(x.to(DEV).permute(0, 2, 3, 1), y, flip_w=flip, y_amax=ya)
     torch.cuda.synchronize()
     ref = x.flip(3) if flip else x
     got = y.cpu()
     assert torch.equal(got[..., :3], ref.permute(0, 2, 3, 1))
     assert torch.equal(got[..., 3:], torch.zeros_like(got[..., 3:]))
-    assert ya.item() == x.abs().max().item()
+    assert torch.equal(ya.cpu(), frame_amax(x))                # per-frame max|y|
     # the border is untouched
     assert torch.equal(buf[:, :3].cpu(), torch.full_like(buf[:, :3].cpu(), 7.0))

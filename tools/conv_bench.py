@@ -74,8 +74,8 @@ def main():
         y = torch.empty(B, Ho, Wo, Co, device=dev)
         r = torch.rand(B, Ho, Wo, Co, device=dev) if "res" in flags else None
         fl = 2.0 * B * Ho * Wo * Co * Ci * k * k
-        xa = x.abs().max().view(1)
-        ya = torch.zeros(1, device=dev) if a.amax else None
+        xa = x.abs().flatten(1).amax(1).contiguous()
+        ya = torch.zeros(x.shape[0], device=dev) if a.amax else None
         for (ko, pk) in pks.items():
           for prec in [int(v) for v in a.prec.split(",")]:
             for tile in [int(v) for v in a.tiles.split(",")]:
