@@ -206,7 +206,9 @@ int prpe_l2norm(const float* x, float* emb, float* norm, int32_t rows, int32_t C
  * score order (ties by index), <= max_nms candidates, class offset 7680*cls,
  * greedy suppression IoU > iou (torchvision.ops.nms), <= max_det kept.
  * out: [B, max_det, 6] (x1,y1,x2,y2,conf,cls), count: [B] int32. No host sync.
- * workspace: >= prpe_nms_workspace_bytes(B, N, nc, max_nms) bytes.
+ * workspace: >= prpe_nms_workspace_bytes(B, N, nc, max_nms) bytes, 256-B aligned (0 bytes and
+ * NULL allowed when N*nc <= 16384: candidates sorted in LDS; above that the keys and one
+ * rocPRIM radix sort per image go through the workspace).
  * The reference's wall-clock cut-off (util.py:133-134,166-167) is not reproduced.
  */
 int64_t prpe_nms_workspace_bytes(int32_t B, int32_t N, int32_t nc, int32_t max_nms);

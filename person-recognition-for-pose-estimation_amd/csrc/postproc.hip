@@ -10,8 +10,8 @@
 //   3. greedy suppression by one wavefront against the kept list (<= max_det boxes, LDS):
 //      each lane tests a slice of the kept boxes, __ballot decides; keep until max_det.
 // More candidate pairs than the LDS key array holds (N*nc > 16384, e.g. a raw 80-class
-// output) take the global path: keys into the caller's workspace, a rocPRIM segmented radix
-// sort (stable, one segment per image), then the same greedy pass.
+// output) take the global path: keys into the caller's workspace, a rocPRIM radix
+// (one rocPRIM device radix sort per image), then the same greedy pass.
 // IoU in fp32 exactly as torchvision's CPU kernel (boxes offset by 7680*cls first,
 // area = (x2-x1)*(y2-y1), inter / (area_i + area_j - inter) > thr). FP contraction is off
 // in this file so every product/sum rounds like the reference.
@@ -40,9 +40,9 @@ struct NmsK {
   const float* pred; int B, N, nc; int64_t s_img, s_c, s_a;
   float conf, iou; int max_nms, max_det;
   float* out; int* count;
-  unsigned long long* gkeys;          // global path: [B][N*nc] unsorted keys, then the sort input
+  unsigned long long* gkeys;          // global path: [B][N*nc] keys (unused tail = ~0: sorts last)
   const unsigned long long* gsorted;  // global path: [B][N*nc] sorted keys
-  unsigned* seg;                      // global path: [B+1]... begin [B], end [B] offsets
+  int* gtotal;                        // global path: [B] candidate count per image
 };
 
 __device__ __forceinline__ float pred_at(const NmsK& p, int b, int c, int a) {
@@ -223,24 +223,24 @@ __global__ __launch_bounds__(NMS_THREADS) void nms_kernel(NmsK p) {
   nms_greedy(p, b, keys, total < p.max_nms ? total : p.max_nms, L, s_total > NMS_MAX_CAND);
 }
 
-// global path, step 1: enumerate into the workspace; segment offsets for the sort
+// global path, step 1: enumerate into the workspace, pad the image's key range with ~0
+// (sorts after every real key), record the count
 __global__ __launch_bounds__(NMS_THREADS) void nms_enum_global_kernel(NmsK p) {
   __shared__ int wsum[NMS_THREADS / 64];
   const int b = blockIdx.x;
-  const int64_t npairs = (int64_t)p.N * p.nc;
-  const int total = nms_enumerate(p, b, p.gkeys + (int64_t)b * npairs, (int)npairs, wsum);
-  if (threadIdx.x == 0) {
-    p.seg[b] = (unsigned)(b * npairs);
-    p.seg[p.B + b] = (unsigned)(b * npairs + total);
-  }
+  const int npairs = p.N * p.nc;
+  unsigned long long* keys = p.gkeys + (int64_t)b * npairs;
+  const int total = nms_enumerate(p, b, keys, npairs, wsum);
+  for (int i = total + (int)threadIdx.x; i < npairs; i += NMS_THREADS) keys[i] = ~0ull;
+  if (threadIdx.x == 0) p.gtotal[b] = total;
 }
 
-// global path, step 3: greedy over the sorted segment (the first min(total, max_nms) keys)
+// global path, step 3: greedy over the image's sorted keys (the first min(total, max_nms))
 __global__ __launch_bounds__(NMS_THREADS) void nms_greedy_global_kernel(NmsK p) {
   __shared__ NmsLds L;
   const int b = blockIdx.x;
-  const int64_t npairs = (int64_t)p.N * p.nc;
-  const int total = (int)(p.seg[p.B + b] - p.seg[b]);
+  const int npairs = p.N * p.nc;
+  const int total = p.gtotal[b];
   nms_greedy(p, b, p.gsorted + (int64_t)b * npairs, total < p.max_nms ? total : p.max_nms, L, false);
 }
 
@@ -305,13 +305,13 @@ __global__ __launch_bounds__(256) void softargmax_kernel(const float* heat, int 
 
 }  // namespace
 
-// global path workspace: keys [B][N*nc] twice (sort input / output), segment offsets, and the
-// rocPRIM segmented radix sort's temporary storage (all 8-B aligned)
-static int64_t nms_sort_temp_bytes(int32_t B, int64_t npairs) {
+// global path workspace (8-B aligned pieces): keys [B][N*nc] (enumerated), sorted keys
+// [B][N*nc], counts [B] (padded to 256 B), and the temporary storage of one rocPRIM device
+// radix sort over N*nc keys (one sort per image: the images' ranges are sorted in turn)
+static int64_t nms_sort_temp_bytes(int64_t npairs) {
   size_t bytes = 0;
-  if (rocprim::segmented_radix_sort_keys((void*)nullptr, bytes, (const unsigned long long*)nullptr,
-                                         (unsigned long long*)nullptr, (size_t)(B * npairs), (unsigned)B,
-                                         (const unsigned*)nullptr, (const unsigned*)nullptr, 0, 64) != hipSuccess)
+  if (rocprim::radix_sort_keys((void*)nullptr, bytes, (const unsigned long long*)nullptr,
+                               (unsigned long long*)nullptr, (size_t)npairs, 0, 64) != hipSuccess)
     return -1;
   return (int64_t)((bytes + 255) / 256 * 256);
 }
@@ -320,9 +320,9 @@ extern "C" int64_t prpe_nms_workspace_bytes(int32_t B, int32_t N, int32_t nc, in
   if (B <= 0 || N <= 0 || nc <= 0) return 0;
   const int64_t npairs = (int64_t)N * nc;
   if (npairs <= NMS_MAX_CAND) return 0;                 // LDS path
-  const int64_t t = nms_sort_temp_bytes(B, npairs);
+  const int64_t t = nms_sort_temp_bytes(npairs);
   if (t < 0) return -1;
-  return 2 * 8 * B * npairs + (int64_t)((2 * B * 4 + 255) / 256 * 256) + t;
+  return 2 * 8 * B * npairs + (int64_t)((4 * B + 255) / 256 * 256) + t;
 }
 
 extern "C" int prpe_nms(const float* pred, int32_t B, int32_t N, int32_t nc, int32_t layout, float conf, float iou,
@@ -331,7 +331,7 @@ extern "C" int prpe_nms(const float* pred, int32_t B, int32_t N, int32_t nc, int
   if (!pred || !out || !count || B <= 0 || N <= 0 || nc <= 0) return PRPE_EINVAL;
   if (max_det <= 0 || max_det > NMS_MAX_DET || max_nms <= 0) return PRPE_EINVAL;
   const int64_t npairs = (int64_t)N * nc;
-  if (npairs >= (1LL << 31) || B * npairs >= (1LL << 32)) return PRPE_EINVAL;
+  if (npairs >= (1LL << 31)) return PRPE_EINVAL;
   NmsK p{};
   p.pred = pred; p.B = B; p.N = N; p.nc = nc;
   if (layout == 0) { p.s_img = (int64_t)(4 + nc) * N; p.s_c = N; p.s_a = 1; }
@@ -346,21 +346,23 @@ extern "C" int prpe_nms(const float* pred, int32_t B, int32_t N, int32_t nc, int
   // global path: more candidate pairs than the LDS holds (e.g. a raw 80-class YOLO output,
   // A = 8400 x nc = 80 at conf 0.001; the reference sorts any count, util.py:157)
   const int64_t need = prpe_nms_workspace_bytes(B, N, nc, max_nms);
-  if (need <= 0 || !workspace || workspace_bytes < need || (uintptr_t)workspace % 8) return PRPE_EINVAL;
+  if (need <= 0 || !workspace || workspace_bytes < need || (uintptr_t)workspace % 256) return PRPE_EINVAL;
   unsigned char* w = static_cast<unsigned char*>(workspace);
   p.gkeys = reinterpret_cast<unsigned long long*>(w);
   unsigned long long* sorted = p.gkeys + B * npairs;
   p.gsorted = sorted;
-  p.seg = reinterpret_cast<unsigned*>(sorted + B * npairs);
-  void* temp = w + 2 * 8 * B * npairs + (2 * B * 4 + 255) / 256 * 256;
-  size_t tb = (size_t)(need - (2 * 8 * B * npairs + (2 * B * 4 + 255) / 256 * 256));
+  p.gtotal = reinterpret_cast<int*>(sorted + B * npairs);
+  const int64_t head = 2 * 8 * B * npairs + (4 * B + 255) / 256 * 256;
+  void* temp = w + head;
   hipLaunchKernelGGL(nms_enum_global_kernel, dim3(B), dim3(NMS_THREADS), 0, st, p);
   int rc = launch_status();
   if (rc) return rc;
-  if (rocprim::segmented_radix_sort_keys(temp, tb, (const unsigned long long*)p.gkeys, sorted, (size_t)(B * npairs),
-                                         (unsigned)B, (const unsigned*)p.seg, (const unsigned*)(p.seg + B), 0, 64,
-                                         st) != hipSuccess)
-    return PRPE_EINVAL;
+  for (int b = 0; b < B; ++b) {
+    size_t tb = (size_t)(need - head);
+    const hipError_t e = rocprim::radix_sort_keys(temp, tb, (const unsigned long long*)(p.gkeys + b * npairs),
+                                                  sorted + b * npairs, (size_t)npairs, 0, 64, st);
+    if (e != hipSuccess) return (int)e;
+  }
   hipLaunchKernelGGL(nms_greedy_global_kernel, dim3(B), dim3(NMS_THREADS), 0, st, p);
   return launch_status();
 }

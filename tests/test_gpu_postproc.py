@@ -47,7 +47,7 @@ def test_nms_matches_reference_golden(case):
 @pytest.mark.parametrize("nc,N,frac,B", [(80, 8400, 0.05, 2), (80, 8400, 0.002, 1), (1, 20000, 1.0, 2)])
 def test_nms_global_path_many_candidates(nc, N, frac, B):
     """N*nc above the LDS key capacity (16384): the global-workspace path (keys + rocPRIM
-    segmented radix sort). A raw 80-class YOLO output at A = 8400 (the reference sorts any
+    radix sort per image). A raw 80-class YOLO output at A = 8400 (the reference sorts any
     count and keeps <= max_nms = 30000, util.py:126,157): 5 % of the pairs pass conf ->
     33,600 candidates > max_nms, so the truncation is exercised too. Bit-exact vs the oracle."""
     g = torch.Generator().manual_seed(nc * 7 + B)
