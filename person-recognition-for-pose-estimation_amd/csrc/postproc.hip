@@ -10,8 +10,8 @@
 //   3. greedy suppression by one wavefront against the kept list (<= max_det boxes, LDS):
 //      each lane tests a slice of the kept boxes, __ballot decides; keep until max_det.
 // More candidate pairs than the LDS key array holds (N*nc > 16384, e.g. a raw 80-class
-// output) take the global path: keys into the caller's workspace, a rocPRIM radix
-// (one rocPRIM device radix sort per image), then the same greedy pass.
+// output) take the global path: keys into the caller's workspace, one rocPRIM device radix
+// sort per image, then the same greedy pass.
 // IoU in fp32 exactly as torchvision's CPU kernel (boxes offset by 7680*cls first,
 // area = (x2-x1)*(y2-y1), inter / (area_i + area_j - inter) > thr). FP contraction is off
 // in this file so every product/sum rounds like the reference.
