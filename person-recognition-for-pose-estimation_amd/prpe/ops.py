@@ -18,7 +18,17 @@ def _stream() -> C.c_void_p:
 
 
 def _ptr(t) -> int | None:
-    return None if t is None else t.data_ptr()
+    return None if t is None else _gpu(t).data_ptr()
+
+
+def _gpu(*ts):
+    """Every tensor handed to the library must live in device memory: a host pointer in a
+    kernel is a GPU memory fault, so it is refused here, before the C ABI."""
+    for t in ts:
+        if t is not None and not (isinstance(t, torch.Tensor) and t.is_cuda):
+            raise ValueError(f"prpe: expected a HIP device tensor, got {type(t).__name__} on "
+                             f"{getattr(t, 'device', '?')}")
+    return ts[0] if len(ts) == 1 else ts
 
 
 def view(t: torch.Tensor | None) -> View:
@@ -44,6 +54,7 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
     per frame (e.g. the ``y_amax`` its producer raised). ``y_amax`` (any precision): [N] device
     tensor the kernel raises to max|y[n]| per frame (zero it first)."""
     d = ConvDesc()
+    _gpu(pack.w_hi)
     N = x.shape[0]
     for a in (x_amax, y_amax, x2_amax):
         if a is not None and (a.dtype != torch.float32 or not a.is_cuda or a.numel() < N or not a.is_contiguous()):
@@ -88,7 +99,7 @@ def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none"
 
 
 def dwconv(x, y, w, k, stride, pad, scale, bias, act="none", res=None):
-    check(lib().prpe_dwconv(C.byref(view(x)), C.byref(view(y)), C.byref(view(res)), w.data_ptr(), k, stride, pad,
+    check(lib().prpe_dwconv(C.byref(view(x)), C.byref(view(y)), C.byref(view(res)), _ptr(w), k, stride, pad,
                             _ptr(scale), _ptr(bias), ACT[act], _stream()), "prpe_dwconv")
     return y
 
@@ -121,6 +132,7 @@ def norm_sigmoid(x, y):
 
 
 def layernorm(x2d, y2d, gamma, beta, eps=1e-12, relu=False):
+    _gpu(x2d, y2d, gamma, beta)
     rows, c = x2d.shape
     check(lib().prpe_layernorm(x2d.data_ptr(), x2d.stride(0), y2d.data_ptr(), y2d.stride(0), rows, c,
                                gamma.data_ptr(), beta.data_ptr(), eps, 1 if relu else 0, _stream()),
@@ -129,6 +141,7 @@ def layernorm(x2d, y2d, gamma, beta, eps=1e-12, relu=False):
 
 
 def attention(qkv, out, B, L, H, D, scale):
+    _gpu(qkv, out)
     check(lib().prpe_attention(qkv.data_ptr(), out.data_ptr(), B, L, H, D, scale, _stream()), "prpe_attention")
     return out
 
@@ -140,6 +153,7 @@ def psa_attention(qkv, out, vout, nh, dk, dh, scale):
 
 
 def dfl_decode(head, out, nc, level_hw, strides):
+    _gpu(head, out)
     B = head.shape[0]
     hw = (C.c_int32 * (2 * len(level_hw)))(*[v for hw_ in level_hw for v in hw_])
     st = (C.c_float * len(strides))(*[float(s) for s in strides])
@@ -151,6 +165,7 @@ def dfl_decode(head, out, nc, level_hw, strides):
 def l2norm(x, emb, norm, eps=0.0):
     """emb = x / max(||x||, eps) per row, norm = ||x||. eps 0: torch.div(x, norm) (IR-50 output);
     eps 1e-12: F.normalize."""
+    _gpu(x, emb, norm)
     rows, c = x.shape
     check(lib().prpe_l2norm(x.data_ptr(), emb.data_ptr(), norm.data_ptr(), rows, c, float(eps), _stream()),
           "prpe_l2norm")
@@ -159,7 +174,7 @@ def l2norm(x, emb, norm, eps=0.0):
 
 def nms(pred, layout, conf=0.001, iou=0.65, max_nms=30000, max_det=300):
     """Batched device NMS -> (out [B,max_det,6], count [B] int32). layout 0: [B,4+nc,N]; 1: [B,N,4+nc]."""
-    pred = pred.contiguous()
+    pred = _gpu(pred).contiguous()
     B = pred.shape[0]
     if layout == 0:
         nc, N = pred.shape[1] - 4, pred.shape[2]
@@ -167,7 +182,7 @@ def nms(pred, layout, conf=0.001, iou=0.65, max_nms=30000, max_det=300):
         N, nc = pred.shape[1], pred.shape[2] - 4
     out = torch.empty(B, max_det, 6, device=pred.device, dtype=torch.float32)
     cnt = torch.empty(B, device=pred.device, dtype=torch.int32)
-    # N*nc above the kernel's LDS key capacity: keys + segmented sort in a global workspace
+    # N*nc above the kernel's LDS key capacity: keys + a radix sort per image in a global workspace
     nbytes = lib().prpe_nms_workspace_bytes(B, N, nc, max_nms)
     if nbytes < 0:
         raise RuntimeError("prpe_nms_workspace_bytes failed")
@@ -178,7 +193,7 @@ def nms(pred, layout, conf=0.001, iou=0.65, max_nms=30000, max_det=300):
 
 
 def softargmax(heat, boxes=None, want_argmax=False):
-    heat = heat.contiguous()
+    heat = _gpu(heat).contiguous()
     B, K, H, W = heat.shape
     coords = torch.empty(B, K, 2, device=heat.device, dtype=torch.float32)
     scores = torch.empty(B, K, device=heat.device, dtype=torch.float32)
@@ -191,7 +206,7 @@ def softargmax(heat, boxes=None, want_argmax=False):
 
 def flip_average(heat, heat_flipped, partner, mode=0):
     """Pose flip test: (heat + flipback(heat_flipped)) * 0.5 (pose_estimation/module.py:470-484)."""
-    heat, heat_flipped = heat.contiguous(), heat_flipped.contiguous()
+    heat, heat_flipped = (t.contiguous() for t in _gpu(heat, heat_flipped))
     B, K, H, W = heat.shape
     out = torch.empty_like(heat)
     pa = (C.c_int32 * K)(*[int(v) for v in partner])
@@ -202,6 +217,7 @@ def flip_average(heat, heat_flipped, partner, mode=0):
 
 def ce_argmax(logits, labels=None):
     """Per-row argmax (+ cross-entropy and the [mean loss, acc] summary when labels given)."""
+    _gpu(logits)
     B, Cn = logits.shape
     assert logits.stride(1) == 1
     amax = torch.empty(B, device=logits.device, dtype=torch.int32)
@@ -217,6 +233,7 @@ def ce_argmax(logits, labels=None):
 
 def det_metrics_update(dets, counts, gt_boxes, gt_batch, counters, records):
     """Append one batch to the device DetectionMetrics state (see include/prpe.h)."""
+    _gpu(dets, counts, counters, records)
     B, max_det, six = dets.shape
     assert six == 6 and dets.is_contiguous() and counts.dtype == torch.int32
     gt = gt_boxes.to(device=dets.device, dtype=torch.float32).contiguous().view(-1, 4)
@@ -230,6 +247,7 @@ def det_metrics_update(dets, counts, gt_boxes, gt_batch, counters, records):
 
 def det_metrics_compute(counters, records, n, thresholds):
     """(precision, recall, f1, mAP50, mAP75, mAP) as a float64 device tensor [6]."""
+    _gpu(counters, records)
     nbytes = lib().prpe_det_metrics_compute_workspace_bytes(n)
     ws = torch.empty((nbytes + 3) // 4, device=counters.device, dtype=torch.float32)
     out = torch.empty(6, device=counters.device, dtype=torch.float64)
@@ -242,6 +260,7 @@ def det_metrics_compute(counters, records, n, thresholds):
 def det_eval_loss(boxes, scores, gt_boxes, gt_batch, gt_classes=None):
     """Detection eval loss (see include/prpe.h): boxes [B,4,N], scores [B,C,N] (any strides).
     Returns (loss [1], per_image [B,4] = (loss_b, box, cls, bg))."""
+    _gpu(boxes, scores)
     B, four, N = boxes.shape
     Cn = scores.shape[1]
     assert four == 4 and scores.shape[0] == B and scores.shape[2] == N

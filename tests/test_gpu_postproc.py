@@ -56,13 +56,21 @@ def test_nms_global_path_many_candidates(nc, N, frac, B):
     sc = torch.rand(B, nc, N, generator=g)
     sc = torch.where(torch.rand(B, nc, N, generator=g) < frac, sc * 0.99 + 0.01, sc * 0.0009)
     inp = torch.cat([cxy, wh, sc], 1).contiguous()
-    out, cnt = non_max_suppression_padded(inp)
+    out, cnt = non_max_suppression_padded(inp.cuda())
     torch.cuda.synchronize()
     ref = R.non_max_suppression(inp)
     for i in range(B):
         assert cnt[i].item() == len(ref[i])
         np.testing.assert_array_equal(out[i, :cnt[i]].cpu().numpy(), ref[i].numpy())
     assert min(len(r) for r in ref) > 0
+
+
+def test_host_tensors_are_refused_before_the_abi():
+    """A host pointer in a kernel is a GPU memory fault: every wrapper refuses CPU tensors."""
+    with pytest.raises(ValueError, match="device tensor"):
+        non_max_suppression_padded(torch.rand(1, 5, 20000))
+    with pytest.raises(ValueError, match="device tensor"):
+        keypoints_from_heatmaps(torch.rand(1, 17, 64, 48))
 
 
 def test_nms_list_api_and_transposed_layout():
