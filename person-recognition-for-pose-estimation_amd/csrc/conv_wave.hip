@@ -263,6 +263,24 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
   }
   FrameMax ymax;                                      // per-frame running max|y| (p.y_amax)
+  // Frame of an output row without a division per row: the wave's rows [wrow0, wrow0 + WTM)
+  // start in frame nf0 (wave-uniform) and, when a frame holds at least WTM rows, reach at most
+  // into frame nf0 + 1 (rows >= nb); smaller frames fall back to m / HoWo. The precision-3
+  // inverse activation scales of those two frames are read once.
+  const bool track = F16 || p.y_amax;
+  const int nf0 = track ? wrow0 / p.HoWo : 0;
+  const int nb = (nf0 + 1) * p.HoWo;
+  const bool two = p.HoWo >= WTM;
+  float inv0 = 1.f, inv1 = 1.f;
+  if constexpr (F16) {
+    auto inv_of = [&](int n) {
+      const float am = DUAL ? fmaxf(p.x_amax[n], p.x2_amax[n]) : p.x_amax[n];
+      return ldexpf(1.f, f16_scale_exp(am) - 15);     // 2^(e - 15) of the frame: exact
+    };
+    if (wrow0 < p.M) inv0 = inv_of(nf0);
+    if (nb < p.M) inv1 = inv_of(nf0 + 1);
+  }
+  auto frame_of = [&](int m) { return two ? nf0 + (m >= nb) : m / p.HoWo; };
   auto offs = [&](int m, int64_t& yo, int64_t& ro) {
     if (p.ylin && p.rlin) {
       yo = (int64_t)m * p.ysw + col;
@@ -297,16 +315,20 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
         int64_t ro;
         offs(m, yo[e], ro);
         if (p.res_mode != PRPE_RES_NONE) res[e] = *reinterpret_cast<const f4*>(p.r + ro);
-        if (F16 || p.y_amax) fn[e] = m / p.HoWo;
+        if (track) fn[e] = frame_of(m);
       }
     }
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
       f4 v = *reinterpret_cast<const f4*>(ct + (rr0 + RPP * e) * CS + cc * 4);
       if (!ok[e]) continue;
-      if constexpr (F16) {                            // 2^(e - 15) of the row's frame: exact
-        const float am = DUAL ? fmaxf(p.x_amax[fn[e]], p.x2_amax[fn[e]]) : p.x_amax[fn[e]];
-        v = v * ldexpf(1.f, f16_scale_exp(am) - 15);
+      if constexpr (F16) {
+        if (two) {
+          v = v * (fn[e] == nf0 ? inv0 : inv1);
+        } else {
+          const float am = DUAL ? fmaxf(p.x_amax[fn[e]], p.x2_amax[fn[e]]) : p.x_amax[fn[e]];
+          v = v * ldexpf(1.f, f16_scale_exp(am) - 15);
+        }
       }
       v = v * sc4 + bi4;
       if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];

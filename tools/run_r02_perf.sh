@@ -1,0 +1,12 @@
+#!/bin/bash
+# GPU-box script: conv op tests, per-layer profile (bs=256), one full bench line
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+TAG=${1:-perf}; shift
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_batch.py -x -q --timeout 200 --timeout-method thread > gpurun_out/${TAG}_ops.log 2>&1 || { tail -40 gpurun_out/${TAG}_ops.log; exit 1; }
+tail -1 gpurun_out/${TAG}_ops.log
+timeout -k 10 300 python tools/layer_profile.py --batch 256 "$@" > gpurun_out/${TAG}_layer_profile.txt 2>&1 || { tail -30 gpurun_out/${TAG}_layer_profile.txt; exit 1; }
+head -3 gpurun_out/${TAG}_layer_profile.txt; tail -2 gpurun_out/${TAG}_layer_profile.txt
+timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/${TAG}_bench.json'));print(d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])"
