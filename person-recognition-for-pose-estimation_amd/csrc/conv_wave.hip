@@ -79,6 +79,19 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   int64_t rbase2[DUAL ? TM : 1];
   unsigned hmask[TM], wmask[TM];
   float sa[F16 ? TM : 1];                             // precision 3: per-row (= per-frame) scale
+  // A wave's rows [wrow0, wrow0 + WTM) start in frame nf0 and, when a frame holds at least WTM
+  // rows ("two"), reach at most into frame nf0 + 1 (rows >= nb): the frame of a row is one
+  // compare, and the two frames' max|x| bounds are wave-uniform (scalar) loads.
+  const int nf0 = wrow0 / p.HoWo;
+  const int nb = (nf0 + 1) * p.HoWo;
+  const bool two = p.HoWo >= WTM;
+  float am0 = 0.f, am1 = 0.f;                         // max|x| of frames nf0, nf0 + 1 (F16)
+  if constexpr (F16) {
+    if (two) {
+      if (wrow0 < p.M) am0 = DUAL ? fmaxf(p.x_amax[nf0], p.x2_amax[nf0]) : p.x_amax[nf0];
+      if (nb < p.M) am1 = DUAL ? fmaxf(p.x_amax[nf0 + 1], p.x2_amax[nf0 + 1]) : p.x_amax[nf0 + 1];
+    }
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wrow0 + i * 16 + fr;
@@ -91,7 +104,8 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       if constexpr (F16) {
         // activation scale of this row's frame: max|x| < 2^e -> 2^(15 - e); a dual GEMM's two
         // inputs share one scale (their per-frame maxima combined)
-        const float am = DUAL ? fmaxf(p.x_amax[n], p.x2_amax[n]) : p.x_amax[n];
+        const float am = two ? (m >= nb ? am1 : am0)
+                             : (DUAL ? fmaxf(p.x_amax[n], p.x2_amax[n]) : p.x_amax[n]);
         sa[i] = ldexpf(1.f, 15 - f16_scale_exp(am));
       }
       const int rem = m - n * p.HoWo;
@@ -262,23 +276,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     if (p.bias) bi4 = *reinterpret_cast<const f4*>(p.bias + col);
     if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
   }
-  FrameMax ymax;                                      // per-frame running max|y| (p.y_amax)
-  // Frame of an output row without a division per row: the wave's rows [wrow0, wrow0 + WTM)
-  // start in frame nf0 (wave-uniform) and, when a frame holds at least WTM rows, reach at most
-  // into frame nf0 + 1 (rows >= nb); smaller frames fall back to m / HoWo. The precision-3
-  // inverse activation scales of those two frames are read once.
+  // per-frame max|y| (p.y_amax): with "two" a running maximum per frame (nf0, nf0 + 1) and
+  // one wave reduction each at the end; else per-lane frame tracking (FrameMax)
   const bool track = F16 || p.y_amax;
-  const int nf0 = track ? wrow0 / p.HoWo : 0;
-  const int nb = (nf0 + 1) * p.HoWo;
-  const bool two = p.HoWo >= WTM;
-  float inv0 = 1.f, inv1 = 1.f;
+  float ym0 = 0.f, ym1 = 0.f;
+  FrameMax ymax;
+  float inv0 = 1.f, inv1 = 1.f;                       // 2^(e - 15) of frames nf0, nf0 + 1: exact
   if constexpr (F16) {
-    auto inv_of = [&](int n) {
-      const float am = DUAL ? fmaxf(p.x_amax[n], p.x2_amax[n]) : p.x_amax[n];
-      return ldexpf(1.f, f16_scale_exp(am) - 15);     // 2^(e - 15) of the frame: exact
-    };
-    if (wrow0 < p.M) inv0 = inv_of(nf0);
-    if (nb < p.M) inv1 = inv_of(nf0 + 1);
+    inv0 = ldexpf(1.f, f16_scale_exp(am0) - 15);
+    inv1 = ldexpf(1.f, f16_scale_exp(am1) - 15);
   }
   auto frame_of = [&](int m) { return two ? nf0 + (m >= nb) : m / p.HoWo; };
   auto offs = [&](int m, int64_t& yo, int64_t& ro) {
@@ -325,7 +331,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       if constexpr (F16) {
         if (two) {
           v = v * (fn[e] == nf0 ? inv0 : inv1);
-        } else {
+        } else {                                      // frames smaller than a wave tile
           const float am = DUAL ? fmaxf(p.x_amax[fn[e]], p.x2_amax[fn[e]]) : p.x_amax[fn[e]];
           v = v * ldexpf(1.f, f16_scale_exp(am) - 15);
         }
@@ -345,10 +351,25 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       } else {
         *reinterpret_cast<f4*>(p.y + yo[e]) = v;
       }
-      if (p.y_amax) ymax.add(p.y_amax, fn[e], amax4(v));
+      if (p.y_amax) {
+        const float a = amax4(v);
+        if (two) {
+          ym0 = fmaxf(ym0, fn[e] == nf0 ? a : 0.f);
+          ym1 = fmaxf(ym1, fn[e] == nf0 ? 0.f : a);
+        } else {
+          ymax.add(p.y_amax, fn[e], a);
+        }
+      }
     }
   }
-  if (p.y_amax) frame_amax_final(p.y_amax, ymax);
+  if (p.y_amax) {
+    if (two) {
+      if (wrow0 < p.M) amax_commit(p.y_amax + nf0, ym0);
+      if (nb < p.M) amax_commit(p.y_amax + nf0 + 1, ym1);
+    } else {
+      frame_amax_final(p.y_amax, ymax);
+    }
+  }
 }
 
 template <int NW, int TM, int TN, int NP, int STAGES, bool F16 = false>
