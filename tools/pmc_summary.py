@@ -45,8 +45,11 @@ def main():
         if "SQ_INSTS_LDS" in g and "SQ_LDS_BANK_CONFLICT" in g and "SQ_LDS_IDX_ACTIVE" in g and g["SQ_LDS_IDX_ACTIVE"]:
             print(f"   {'LDS bank-conflict / LDS active':40s} {g['SQ_LDS_BANK_CONFLICT'] / g['SQ_LDS_IDX_ACTIVE']:8.3f}")
         if "SQ_VALU_MFMA_BUSY_CYCLES" in g and "GRBM_GUI_ACTIVE" in g and g["GRBM_GUI_ACTIVE"]:
-            print(f"   {'MFMA busy / (GUI_ACTIVE * 256 CU * 4 SIMD)':40s} "
-                  f"{g['SQ_VALU_MFMA_BUSY_CYCLES'] / (g['GRBM_GUI_ACTIVE'] * 1024):8.3f}")
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back);
+            # SQ_VALU_MFMA_BUSY_CYCLES = 16 x the 16x16x32 MFMAs issued (matrix-pipe cycles, all SIMDs)
+            gui = g["GRBM_GUI_ACTIVE"] / 8
+            print(f"   {'MFMA busy / (GUI_ACTIVE/8 * 1024 SIMD)':40s} {g['SQ_VALU_MFMA_BUSY_CYCLES'] / (gui * 1024):8.3f}")
+            print(f"   {'effective clock GHz (GUI_ACTIVE/8 / dur)':40s} {gui / (sum(d) / len(d) * 1e3):8.3f}")
 
 
 if __name__ == "__main__":
