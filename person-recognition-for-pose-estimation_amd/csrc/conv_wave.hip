@@ -246,6 +246,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   issue_b(0, 0);
   if constexpr (STAGES == 3) issue_b(nk > 1 ? 1 : 0, 1);
   split_a();
+  // planes input: the A fragments of step 0 ARE the load destinations (no split), so the
+  // compiler's wait bookkeeping would carry their pending loads into the loop header and merge
+  // them into a vmcnt(0) before every K-step's first MFMA (tools/loop_waits.py) -- i.e. every
+  // step would wait for the A(kt+1) loads and B DMA it had just issued. Retiring the prologue
+  // loads here with a wait the compiler can see costs one latency per block, and the loop keeps
+  // its overlap (STAGES 2 waits for them at the loop top anyway).
+  if constexpr (APL) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
   int st = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // B(kt) of this wave: at most the (STAGES-2)*IB pieces issued after it are still pending
