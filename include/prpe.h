@@ -178,6 +178,16 @@ int prpe_layernorm(const float* x, int64_t x_row_stride, float* y, int64_t y_row
 int prpe_attention(const float* qkv, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
                    float scale, void* stream);
 
+/* The same attention on a strided q/k/v operand: element (frame b, which w = 0 q / 1 k / 2 v,
+ * head h, token t, channel d) at qkv[b*s_frame + w*s_which + h*s_head + t*s_tok + d]; all
+ * strides multiples of 4 elements, qkv 16-B aligned. prpe_attention is the row-major case
+ * (s_frame = L*3*H*D, s_which = H*D, s_head = D, s_tok = 3*H*D); a head-major QKV GEMM output
+ * [B][3][H][L][D] (s_frame = 3*H*L*D, s_which = H*L*D, s_head = L*D, s_tok = D) gives every
+ * head's K and V as one contiguous 48-KB block. out: [B*L][H*D]. */
+int prpe_attention_strided(const float* qkv, int64_t s_frame, int64_t s_which, int64_t s_head,
+                           int64_t s_tok, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
+                           float scale, void* stream);
+
 /* YOLO PSA attention core (nn.py:111-122): per frame, per head:
  *   out[c, i] = sum_j v[c, j] softmax_j(q[:, i] . k[:, j] * scale)
  * qkv view [N, h, w, nh*(2*dk+dh)] (per head: q dk | k dk | v dh), out view [N,h,w,nh*dh].

@@ -13,6 +13,7 @@
 // prpe_psa_attention — YOLO v11 PSA attention core (nn.py:111-122), 25 tokens, 2 heads;
 // tiny, VALU fp32, one workgroup per frame.
 #include "common.h"
+#include <stdlib.h>
 
 namespace {
 
@@ -157,6 +158,407 @@ __global__ __launch_bounds__(NWAVE * 64) void vit_attention_kernel(const float* 
     }
 }
 
+// ----------------------------------------------------------------------------- v2
+// vit_attention_t_kernel — the same function computed transposed, in key chunks:
+//   S^T = K Q^T   (A = K rows from LDS, B = Q^T: the wave's queries, in registers)
+//   O^T = V^T P^T (A = V^T from LDS, B = P^T straight from the S^T accumulators)
+// The S^T accumulator of a 16-key tile gives lane (fr, fg) keys 4 fg + r of query fr, which is
+// exactly a B-fragment of P^T once the K index of a 32-key PV step is taken in the order
+// (tile 2c: keys 4 fg .. 4 fg + 3, tile 2c + 1: keys 16 + 4 fg .. 16 + 4 fg + 3) -- so P never
+// goes through LDS, and the A-fragment of V^T reads the same two 4-key runs (two 8-B reads).
+// Softmax runs over the rows of S^T (a query's keys: 4 r x 4 lane groups x tiles): two
+// shuffles per reduction. Keys are processed KC at a time with an online-softmax merge
+// (running max m, sum l, rescale of O by exp(m_old - m_new)), so only one chunk of K and V^T is
+// staged: 2 x (KC x 72 + 64 x (KC + 8)) bf16 = 36 KB at KC = 64 instead of 137 KB. A wave owns
+// QT 16-query tiles (each K / V^T fragment read from LDS feeds QT MFMAs); with QT = 2 a
+// workgroup is 6 waves and two or more workgroups share a CU, one staging while another
+// computes. 1 / l once per query at the end; O^T rows are d, so each lane stores 4
+// consecutive channels (16-B stores).
+template <int KC, int QT>
+__global__ __launch_bounds__(AL / 16 / QT * 64) __attribute__((amdgpu_waves_per_eu(QT == 2 ? 3 : 4))) void vit_attention_t_kernel(const float* __restrict__ qkv,
+                                                                           float* __restrict__ out, int H,
+                                                                           float scale) {
+  static_assert(AL % KC == 0 && KC % 32 == 0, "key chunk");
+  constexpr int NW = AL / 16 / QT;         // waves
+  constexpr int NT = NW * 64;
+  constexpr int KT = KC / 16;              // 16-key tiles per chunk
+  constexpr int VR = KC + 8;               // bf16 per V^T row (pad 16 B)
+  constexpr int KSZ = KC * KROW, VSZ = AD * VR;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * KSZ + 2 * VSZ];
+  __bf16* Kh = lds;
+  __bf16* Kl = lds + KSZ;
+  __bf16* Vh = lds + 2 * KSZ;
+  __bf16* Vl = lds + 2 * KSZ + VSZ;
+
+  const int b = blockIdx.x / H, h = blockIdx.x % H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int HD = H * AD;
+  const int64_t rs = 3 * (int64_t)HD;
+  const float* base = qkv + (int64_t)b * AL * rs;
+  const int q0 = wave * 16 * QT;
+
+  // Q^T B-fragments: lane (fr = query, fg) holds d = 32 ks + 8 fg .. + 7
+  bf16x8 qh[QT][2], ql[QT][2];
+#pragma unroll
+  for (int u = 0; u < QT; ++u) {
+    const float* qr = base + (int64_t)(q0 + u * 16 + fr) * rs + h * AD;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const float4 a = *reinterpret_cast<const float4*>(qr + ks * 32 + fg * 8);
+      const float4 c = *reinterpret_cast<const float4*>(qr + ks * 32 + fg * 8 + 4);
+      const float v[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __bf16 hi, lo;
+        split_bf16(v[j], hi, lo);
+        qh[u][ks][j] = hi; ql[u][ks][j] = lo;
+      }
+    }
+  }
+
+  float m[QT], l[QT];                      // running max / sum of query fr of tile u
+  f32x4 o[QT][4];
+#pragma unroll
+  for (int u = 0; u < QT; ++u) {
+    m[u] = -1e30f; l[u] = 0.f;          // finite: exp_hw(-inf) would be NaN
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[u][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+
+  for (int c0 = 0; c0 < AL; c0 += KC) {
+    if (c0) __syncthreads();               // every wave done with the previous chunk
+    // K rows [key][d] as hi/lo: one float4 per item, 8-B LDS writes
+    for (int i = tid; i < KC * (AD / 4); i += NT) {
+      const int key = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+      const float4 k4 = *reinterpret_cast<const float4*>(base + (c0 + key) * rs + HD + h * AD + d4);
+      const float kv[4] = {k4.x, k4.y, k4.z, k4.w};
+      bf16x4 khi, klo;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        __bf16 hi, lo;
+        split_bf16(kv[j], hi, lo);
+        khi[j] = hi; klo[j] = lo;
+      }
+      *reinterpret_cast<bf16x4*>(Kh + key * KROW + d4) = khi;
+      *reinterpret_cast<bf16x4*>(Kl + key * KROW + d4) = klo;
+    }
+    // V^T [d][key]: an item is 4 keys x 4 channels (four float4 loads; 16 consecutive threads
+    // cover one key's 64 channels), transposed in registers, 8-B LDS writes of 4 keys
+    for (int i = tid; i < (KC / 4) * (AD / 4); i += NT) {
+      const int k4 = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+      float v[4][4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const float4 t = *reinterpret_cast<const float4*>(base + (c0 + k4 * 4 + kk) * rs + 2 * HD + h * AD + d4);
+        v[kk][0] = t.x; v[kk][1] = t.y; v[kk][2] = t.z; v[kk][3] = t.w;
+      }
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) {
+        bf16x4 vhi, vlo;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          __bf16 hi, lo;
+          split_bf16(v[kk][dd], hi, lo);
+          vhi[kk] = hi; vlo[kk] = lo;
+        }
+        *reinterpret_cast<bf16x4*>(Vh + (d4 + dd) * VR + k4 * 4) = vhi;
+        *reinterpret_cast<bf16x4*>(Vl + (d4 + dd) * VR + k4 * 4) = vlo;
+      }
+    }
+    __syncthreads();
+
+    // S^T tiles: rows = keys c0 + 16 t + 4 fg + r, column = query q0 + 16 u + fr
+    f32x4 s[QT][KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+#pragma unroll
+      for (int u = 0; u < QT; ++u) s[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int off = (t * 16 + fr) * KROW + ks * 32 + fg * 8;
+        const bf16x8 kh = *reinterpret_cast<const bf16x8*>(Kh + off);
+        const bf16x8 kl = *reinterpret_cast<const bf16x8*>(Kl + off);
+#pragma unroll
+        for (int u = 0; u < QT; ++u) {
+          s[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qh[u][ks], s[u][t], 0, 0, 0);
+          s[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, ql[u][ks], s[u][t], 0, 0, 0);
+          s[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, qh[u][ks], s[u][t], 0, 0, 0);
+        }
+      }
+    }
+    // online softmax over this chunk's keys, per query
+#pragma unroll
+    for (int u = 0; u < QT; ++u) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { s[u][t][r] *= scale; mx = fmaxf(mx, s[u][t][r]); }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[u], mx);
+      const float alpha = exp_hw(m[u] - mn);   // 0 on the first chunk (m = -1e30)
+      m[u] = mn;
+      float sum = 0.f;
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { const float e = exp_hw(s[u][t][r] - mn); s[u][t][r] = e; sum += e; }
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      l[u] = l[u] * alpha + sum;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[u][j] *= alpha;
+    }
+
+    // O^T += V^T P^T, 32 keys per step
+#pragma unroll
+    for (int c = 0; c < KT / 2; ++c) {
+      bf16x8 ph[QT], pl[QT];
+#pragma unroll
+      for (int u = 0; u < QT; ++u)
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          __bf16 hi, lo;
+          split_bf16(s[u][2 * c + (jj >> 2)][jj & 3], hi, lo);
+          ph[u][jj] = hi; pl[u][jj] = lo;
+        }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int off = (j * 16 + fr) * VR + c * 32 + fg * 4;
+        const bf16x4 h0 = *reinterpret_cast<const bf16x4*>(Vh + off);
+        const bf16x4 h1 = *reinterpret_cast<const bf16x4*>(Vh + off + 16);
+        const bf16x4 l0 = *reinterpret_cast<const bf16x4*>(Vl + off);
+        const bf16x4 l1 = *reinterpret_cast<const bf16x4*>(Vl + off + 16);
+        const bf16x8 vh = {h0[0], h0[1], h0[2], h0[3], h1[0], h1[1], h1[2], h1[3]};
+        const bf16x8 vl = {l0[0], l0[1], l0[2], l0[3], l1[0], l1[1], l1[2], l1[3]};
+#pragma unroll
+        for (int u = 0; u < QT; ++u) {
+          o[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, ph[u], o[u][j], 0, 0, 0);
+          o[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, pl[u], o[u][j], 0, 0, 0);
+          o[u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, ph[u], o[u][j], 0, 0, 0);
+        }
+      }
+    }
+  }
+  // out[b*L + q][h*D + d], d = 16 j + 4 fg + r: one 16-B store per tile
+#pragma unroll
+  for (int u = 0; u < QT; ++u) {
+    const float inv = __builtin_amdgcn_rcpf(l[u]);
+    float* orow = out + ((int64_t)b * AL + q0 + u * 16 + fr) * HD + h * AD + fg * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(orow + j * 16) = o[u][j] * inv;
+  }
+}
+
+// ----------------------------------------------------------------------------- v3
+// vit_attention_s_kernel — the transposed chunked kernel above (QT = 1, 12 waves) as a
+// software pipeline over a STREAM of (head, key-chunk) items: a workgroup owns `hpw` heads of
+// one frame and walks their 192 / KC chunks each; the fp32 K / V (and, at a head's first
+// chunk, Q) of item i + 1 are loaded into registers while item i computes, and written to LDS
+// (split into planes) after the barrier that retires item i's reads. Only the very first
+// item's loads are exposed; the kernel reads q, k, v once and writes o once, so it is bound by
+// that HBM traffic (4 x 4 B x L x H x D per frame), not by the MFMAs.
+// element strides of the q / k / v operand: frame, q->k->v, head, token (channel stride 1)
+struct AttnStrides {
+  int64_t frame, which, head, tok;
+};
+
+template <int KC>
+__global__ __launch_bounds__(NWAVE * 64) void vit_attention_s_kernel(const float* __restrict__ qkv, AttnStrides sd,
+                                                                    float* __restrict__ out, int H, int hpw,
+                                                                    float scale) {
+  static_assert(AL % KC == 0 && KC % 32 == 0, "key chunk");
+  constexpr int NT = NWAVE * 64;
+  constexpr int NCH = AL / KC;
+  constexpr int KT = KC / 16;
+  constexpr int VR = KC + 8;
+  constexpr int KSZ = KC * KROW, VSZ = AD * VR;
+  constexpr int KN = KC * (AD / 4);                      // float4 of K per chunk
+  constexpr int VN = (KC / 4) * (AD / 4);                // 4x4 V items per chunk
+  constexpr int KPT = (KN + NT - 1) / NT, VPT = (VN + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * KSZ + 2 * VSZ];
+  __bf16* Kh = lds;
+  __bf16* Kl = lds + KSZ;
+  __bf16* Vh = lds + 2 * KSZ;
+  __bf16* Vl = lds + 2 * KSZ + VSZ;
+
+  const int groups = H / hpw;
+  const int b = blockIdx.x / groups, h0 = (blockIdx.x % groups) * hpw;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int HD = H * AD;
+  const int64_t rs = sd.tok;
+  const float* base = qkv + (int64_t)b * sd.frame;
+  const int q0 = wave * 16;
+  const int nit = hpw * NCH;
+
+  // register stage of one item
+  float4 kr[KPT], vr[VPT][4], qr[4];
+  auto fetch = [&](int it) {
+    const int hh = h0 + it / NCH, c0 = (it % NCH) * KC;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int i = tid + j * NT;
+      if (i < KN) {
+        const int key = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+        kr[j] = *reinterpret_cast<const float4*>(base + (c0 + key) * rs + sd.which + hh * sd.head + d4);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int i = tid + j * NT;
+      if (i < VN) {
+        const int k4 = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk)
+          vr[j][kk] = *reinterpret_cast<const float4*>(base + (c0 + k4 * 4 + kk) * rs + 2 * sd.which + hh * sd.head +
+                                                      d4);
+      }
+    }
+    if (it % NCH == 0) {
+      const float* q = base + (int64_t)(q0 + fr) * rs + hh * sd.head;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        qr[2 * ks] = *reinterpret_cast<const float4*>(q + ks * 32 + fg * 8);
+        qr[2 * ks + 1] = *reinterpret_cast<const float4*>(q + ks * 32 + fg * 8 + 4);
+      }
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int i = tid + j * NT;
+      if (i < KN) {
+        const int key = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+        const float kv[4] = {kr[j].x, kr[j].y, kr[j].z, kr[j].w};
+        bf16x4 khi, klo;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          __bf16 hi, lo;
+          split_bf16(kv[e], hi, lo);
+          khi[e] = hi; klo[e] = lo;
+        }
+        *reinterpret_cast<bf16x4*>(Kh + key * KROW + d4) = khi;
+        *reinterpret_cast<bf16x4*>(Kl + key * KROW + d4) = klo;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int i = tid + j * NT;
+      if (i < VN) {
+        const int k4 = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+#pragma unroll
+        for (int dd = 0; dd < 4; ++dd) {
+          bf16x4 vhi, vlo;
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            __bf16 hi, lo;
+            split_bf16(vr[j][kk][dd], hi, lo);
+            vhi[kk] = hi; vlo[kk] = lo;
+          }
+          *reinterpret_cast<bf16x4*>(Vh + (d4 + dd) * VR + k4 * 4) = vhi;
+          *reinterpret_cast<bf16x4*>(Vl + (d4 + dd) * VR + k4 * 4) = vlo;
+        }
+      }
+    }
+  };
+
+  bf16x8 qh[2], ql[2];
+  float m = -1e30f, l = 0.f;                             // finite: exp_hw(-inf) would be NaN
+  f32x4 o[4];
+  fetch(0);
+  for (int it = 0; it < nit; ++it) {
+    const int c = it % NCH;
+    if (c == 0) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const float v[8] = {qr[2 * ks].x, qr[2 * ks].y, qr[2 * ks].z, qr[2 * ks].w,
+                            qr[2 * ks + 1].x, qr[2 * ks + 1].y, qr[2 * ks + 1].z, qr[2 * ks + 1].w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          __bf16 hi, lo;
+          split_bf16(v[j], hi, lo);
+          qh[ks][j] = hi; ql[ks][j] = lo;
+        }
+      }
+      m = -1e30f; l = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();                                     // item it-1's LDS reads retired
+    stage();
+    if (it + 1 < nit) fetch(it + 1);                     // in flight across this item's MFMAs
+    __syncthreads();
+
+    f32x4 s[KT];
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int off = (t * 16 + fr) * KROW + ks * 32 + fg * 8;
+        const bf16x8 kh = *reinterpret_cast<const bf16x8*>(Kh + off);
+        const bf16x8 kl = *reinterpret_cast<const bf16x8*>(Kl + off);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qh[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, ql[ks], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, qh[ks], acc, 0, 0, 0);
+      }
+      s[t] = acc;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { s[t][r] *= scale; mx = fmaxf(mx, s[t][r]); }
+    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float mn = fmaxf(m, mx);
+    const float alpha = exp_hw(m - mn);
+    m = mn;
+    float sum = 0.f;
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { const float e = exp_hw(s[t][r] - mn); s[t][r] = e; sum += e; }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    l = l * alpha + sum;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] *= alpha;
+#pragma unroll
+    for (int cc = 0; cc < KT / 2; ++cc) {
+      bf16x8 ph, pl;
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        __bf16 hi, lo;
+        split_bf16(s[2 * cc + (jj >> 2)][jj & 3], hi, lo);
+        ph[jj] = hi; pl[jj] = lo;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int off = (j * 16 + fr) * VR + cc * 32 + fg * 4;
+        const bf16x4 a0 = *reinterpret_cast<const bf16x4*>(Vh + off);
+        const bf16x4 a1 = *reinterpret_cast<const bf16x4*>(Vh + off + 16);
+        const bf16x4 b0 = *reinterpret_cast<const bf16x4*>(Vl + off);
+        const bf16x4 b1 = *reinterpret_cast<const bf16x4*>(Vl + off + 16);
+        const bf16x8 vh = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        const bf16x8 vl = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, ph, o[j], 0, 0, 0);
+        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, pl, o[j], 0, 0, 0);
+        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, ph, o[j], 0, 0, 0);
+      }
+    }
+    if (c == NCH - 1) {
+      const float inv = __builtin_amdgcn_rcpf(l);
+      float* orow = out + ((int64_t)b * AL + q0 + fr) * HD + (h0 + it / NCH) * AD + fg * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(orow + j * 16) = o[j] * inv;
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- PSA
 __device__ __forceinline__ int64_t voff(const prpe_view& v, int n, int hh, int ww, int c) {
   return (int64_t)n * v.sn + (int64_t)hh * v.sh + (int64_t)ww * v.sw + (int64_t)c * v.sc;
@@ -198,14 +600,53 @@ __global__ __launch_bounds__(256) void psa_attention_kernel(prpe_view qkv, prpe_
   }
 }
 
+int attention_launch(const float* qkv, AttnStrides sd, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
+                            float scale, void* stream) {
+  if (!qkv || !out || B <= 0 || H <= 0 || L != AL || D != AD) return PRPE_EINVAL;
+  if ((uintptr_t)qkv % 16 || (uintptr_t)out % 16) return PRPE_EINVAL;
+  if (sd.frame % 4 || sd.which % 4 || sd.head % 4 || sd.tok % 4) return PRPE_EINVAL;
+  // PRPE_ATTN selects the kernel for A/B runs: 1 = the round-1 kernel (P through LDS, all 192
+  // keys staged, 12 waves), KC*10 + QT = transposed kernel with KC-key chunks and QT query tiles
+  // per wave (322, 641, 642, 962); 32 / 64 / 96 = the streaming kernel with that chunk;
+  // default 64. Only the streaming kernel takes strided (e.g. head-major) operands.
+  static const int sel = [] {
+    const char* e = getenv("PRPE_ATTN");
+    return e ? atoi(e) : 64;
+  }();
+  const bool rowmajor = sd.frame == (int64_t)L * 3 * H * D && sd.which == (int64_t)H * D && sd.head == D &&
+                        sd.tok == (int64_t)3 * H * D;
+  const dim3 g(B * H);
+  hipStream_t st = as_stream(stream);
+  // streaming kernel: heads per workgroup = the largest divisor of H that still gives every CU
+  // a workgroup (one 12-wave workgroup per CU at its register count)
+  int hpw = H;
+  while (hpw > 1 && ((int64_t)B * H / hpw < 256 || H % hpw)) --hpw;
+  const dim3 gs(B * H / hpw);
+  switch (rowmajor ? sel : 64) {
+    case 1: hipLaunchKernelGGL(vit_attention_kernel, g, dim3(NWAVE * 64), 0, st, qkv, out, H, scale); break;
+    case 322: hipLaunchKernelGGL((vit_attention_t_kernel<32, 2>), g, dim3(6 * 64), 0, st, qkv, out, H, scale); break;
+    case 641: hipLaunchKernelGGL((vit_attention_t_kernel<64, 1>), g, dim3(12 * 64), 0, st, qkv, out, H, scale); break;
+    case 642: hipLaunchKernelGGL((vit_attention_t_kernel<64, 2>), g, dim3(6 * 64), 0, st, qkv, out, H, scale); break;
+    case 962: hipLaunchKernelGGL((vit_attention_t_kernel<96, 2>), g, dim3(6 * 64), 0, st, qkv, out, H, scale); break;
+    case 32: hipLaunchKernelGGL(vit_attention_s_kernel<32>, gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale); break;
+    case 96: hipLaunchKernelGGL(vit_attention_s_kernel<96>, gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale); break;
+    default: hipLaunchKernelGGL(vit_attention_s_kernel<64>, gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale); break;
+  }
+  return launch_status();
+}
+
 }  // namespace
 
 extern "C" int prpe_attention(const float* qkv, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
                               float scale, void* stream) {
-  if (!qkv || !out || B <= 0 || H <= 0 || L != AL || D != AD) return PRPE_EINVAL;
-  if ((uintptr_t)qkv % 16) return PRPE_EINVAL;
-  hipLaunchKernelGGL(vit_attention_kernel, dim3(B * H), dim3(NWAVE * 64), 0, as_stream(stream), qkv, out, H, scale);
-  return launch_status();
+  const int64_t HD = (int64_t)H * D;
+  return attention_launch(qkv, AttnStrides{(int64_t)L * 3 * HD, HD, D, 3 * HD}, out, B, L, H, D, scale, stream);
+}
+
+extern "C" int prpe_attention_strided(const float* qkv, int64_t s_frame, int64_t s_which, int64_t s_head,
+                                      int64_t s_tok, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
+                                      float scale, void* stream) {
+  return attention_launch(qkv, AttnStrides{s_frame, s_which, s_head, s_tok}, out, B, L, H, D, scale, stream);
 }
 
 extern "C" int prpe_psa_attention(const prpe_view* qkv, const prpe_view* out, const prpe_view* vout, int32_t nh,

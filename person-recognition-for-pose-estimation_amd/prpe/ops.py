@@ -146,6 +146,16 @@ def attention(qkv, out, B, L, H, D, scale):
     return out
 
 
+def attention_strided(qkv, strides, out, B, L, H, D, scale):
+    """qkv: tensor holding q/k/v at element strides (frame, which, head, token), e.g. a
+    head-major [B, 3, H, L, D] buffer: (3*H*L*D, H*L*D, L*D, D)."""
+    _gpu(qkv, out)
+    sf, sw, sh, st = (int(v) for v in strides)
+    check(lib().prpe_attention_strided(qkv.data_ptr(), sf, sw, sh, st, out.data_ptr(), B, L, H, D, scale,
+                                       _stream()), "prpe_attention_strided")
+    return out
+
+
 def psa_attention(qkv, out, vout, nh, dk, dh, scale):
     check(lib().prpe_psa_attention(C.byref(view(qkv)), C.byref(view(out)), C.byref(view(vout)), nh, dk, dh, scale,
                                    _stream()), "prpe_psa_attention")

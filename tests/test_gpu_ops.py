@@ -751,6 +751,37 @@ def test_vit_attention():
     torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=5e-5)
 
 
+def test_vit_attention_online_softmax_rescale():
+    # one key per chunk region made dominant for chosen queries, so the running max jumps in a
+    # late key chunk (the O / l rescale branch is taken with a large factor), plus a query whose
+    # logits are all equal (uniform weights)
+    B, L, H, D = 2, 192, 12, 64
+    qkv = rnd(B * L, 3 * H * D, seed=44, scale=1.0).view(B, L, 3, H, D)
+    for q, key in ((5, 170), (40, 3), (100, 65), (191, 191)):
+        qkv[0, key, 1, 2] = 4.0 * qkv[0, q, 0, 2]        # frame 0, head 2: q . k large
+    qkv[1, 7, 0, 5] = 0.0                                 # frame 1, head 5, query 7: all logits 0
+    qkv = qkv.reshape(B * L, 3 * H * D)
+    out = torch.empty(B * L, H * D, device=DEV)
+    ops.attention(qkv.to(DEV), out, B, L, H, D, D ** -0.5)
+    torch.cuda.synchronize()
+    q, k, v = qkv.view(B, L, 3, H, D).permute(2, 0, 3, 1, 4).double()
+    att = torch.softmax(q @ k.transpose(-1, -2) * D ** -0.5, -1)
+    ref = (att @ v).transpose(1, 2).reshape(B * L, H * D).float()
+    torch.testing.assert_close(out.cpu(), ref, rtol=0, atol=5e-5)
+
+
+def test_vit_attention_head_major_operand_bit_identical():
+    B, L, H, D = 2, 192, 12, 64
+    qkv = rnd(B * L, 3 * H * D, seed=45, scale=2.0).to(DEV)
+    a = torch.empty(B * L, H * D, device=DEV)
+    b = torch.empty(B * L, H * D, device=DEV)
+    ops.attention(qkv, a, B, L, H, D, D ** -0.5)
+    hm = qkv.view(B, L, 3, H, D).permute(0, 2, 3, 1, 4).contiguous()
+    ops.attention_strided(hm, (3 * H * L * D, H * L * D, L * D, D), b, B, L, H, D, D ** -0.5)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b)
+
+
 def test_psa_attention():
     B, nh, dk, dh = 2, 2, 32, 64
     per = 2 * dk + dh

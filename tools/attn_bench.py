@@ -35,9 +35,33 @@ def main():
     ms = e0.elapsed_time(e1) / a.iters
     fl = 4.0 * B * H * L * L * D
     by = 4.0 * B * L * H * D * 4
-    print(f"attention bs={B}: {ms:.3f} ms  alg {fl / ms / 1e9:.1f} TF/s  exec {3 * fl / ms / 1e9:.1f} TF/s  "
+    q, k, v = qkv[: 4 * L].view(4, L, 3, H, D).permute(2, 0, 3, 1, 4).double().cpu()
+    ref = (torch.softmax(q @ k.transpose(-1, -2) * D ** -0.5, -1) @ v).transpose(1, 2).reshape(4 * L, H * D)
+    err = float((out[: 4 * L].double().cpu() - ref).abs().max())
+    print(f"PRPE_ATTN={os.environ.get('PRPE_ATTN', 'default')} max|err| {err:.2e}  attention bs={B}: {ms:.3f} ms  alg {fl / ms / 1e9:.1f} TF/s  exec {3 * fl / ms / 1e9:.1f} TF/s  "
           f"{by / ms / 1e6:.0f} GB/s (q,k,v read + o write)")
+
+
+def head_major(B=256, iters=10):
+    L, H, D = 192, 12, 64
+    qkv = torch.rand(B * L, 3 * H * D, device="cuda") - 0.5
+    hm = qkv.view(B, L, 3, H, D).permute(0, 2, 3, 1, 4).contiguous()
+    del qkv
+    st = (3 * H * L * D, H * L * D, L * D, D)
+    out = torch.empty(B * L, H * D, device="cuda")
+    ops.attention_strided(hm, st, out, B, L, H, D, D ** -0.5)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        ops.attention_strided(hm, st, out, B, L, H, D, D ** -0.5)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    print(f"head-major operand: attention bs={B}: {ms:.3f} ms  {4.0 * B * L * H * D * 4 / ms / 1e6:.0f} GB/s")
 
 
 if __name__ == "__main__":
     main()
+    if os.environ.get("PRPE_ATTN", "64") == "64":
+        head_major()
