@@ -121,4 +121,10 @@ int conv_glds_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 bool conv_wave_eligible(const ConvK& kp, int prec, int km);
 int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 
+// haloed-tile 3x3 kernel (conv_halo.hip): 3x3 / s1 / p1, chunk-major weights, precision 0
+// (fp32 or planes input) or 3; tile 30 = auto, 31..35 force a configuration.
+bool conv_halo_eligible(const ConvK& kp, int prec, int km);
+bool conv_halo_auto(const ConvK& kp, int prec);   // the automatic choice's shape rule
+int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
+
 }  // namespace prpe_k

@@ -1,0 +1,312 @@
+// 3x3 / stride 1 / pad 1 convolution on CDNA4 MFMA with the input tile staged ONCE per
+// 32-channel chunk as a haloed spatial tile in LDS ("halo" kernel).
+//
+// Why (tools/conv_bench.py ablations of the wave-row kernel, profiles/r02_conv_ablation.txt):
+// on the adapters' 3x3 256->128 convs the wave-row kernel spends ~25 % of its time on the A
+// operand's fragment-shaped global loads (each input pixel is fetched once per tap: 9 times)
+// and ~25 % on the B ring's LDS-DMA, i.e. on vector-memory instructions per MFMA, not on
+// bytes. Here a block owns a TR x TC patch of output pixels of one frame (all of them in
+// rows of 16 consecutive pixels) and, per 32-channel chunk, DMAs the (TR+2) x (TC+2) input
+// patch into LDS in full 128-B pixel lines; the 9 taps of the chunk then read their A
+// fragments from that tile (a tap is a shift of the patch). With 8 waves per block the B
+// ring costs 2 DMA pieces per wave and K-step instead of 4, and the halo ~0.6.
+//
+// GEMM view, K order (chunk-major: k = (chunk * 9 + kh * 3 + kw) * 32 + ci % 32), split
+// arithmetic and per-accumulator MFMA order are those of conv_wave.hip, so the result is
+// bit-identical to it (tested).
+//
+// LDS (one array): halo double buffer [2][HQ * 8 px][8 x 16 B] (slot swizzle: logical 16-B
+// slot s of pixel q lives at s ^ ((q >> 1) & 7): 16 consecutive pixels of a fragment read hit
+// 16 distinct (half-row, slot) pairs -- conflict-free ds_read_b128), B ring [2][2 planes][128
+// cols][64 B] (the wave kernel's swizzle). The epilogue slab reuses the halo buffers.
+//
+// Pipeline per K-step kt = (chunk c, tap t), one block barrier each:
+//   vmcnt(0) + s_barrier          -- B(kt) and the halo of chunk c (issued earlier) landed
+//   LDS-DMA B(kt+1) -> other stage, and this wave's share of the halo of chunk c+1 (spread
+//   over the taps of chunk c) -> other halo buffer
+//   A fragments of tap t from the halo of chunk c, B fragments from stage kt&1, MFMAs
+#include "conv.h"
+
+namespace prpe_k {
+namespace {
+
+constexpr int HBK = 32;
+
+template <int NW, int TR, int TC, int TN, bool F16, bool APL>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void conv_halo_kernel(ConvK p, int tiles_w, int tiles_h) {
+  static_assert(TC % 16 == 0 && (TR * TC / 16) % NW == 0, "tile");
+  static_assert(!(F16 && APL), "planes input is precision 0");
+  using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
+  constexpr int TM = TR * TC / 16 / NW;                 // 16-pixel row blocks per wave
+  constexpr int BN = TN * 16, NP = 2;
+  constexpr int HW_ = TC + 2, HP = (TR + 2) * HW_;      // halo pixels
+  constexpr int HQ = (HP + 7) / 8;                      // 1-KiB DMA pieces per halo
+  constexpr int HALO = HQ * 8 * 128;                    // bytes per halo buffer
+  constexpr int B_STAGE = NP * BN * 64;
+  constexpr int NB_TOT = NP * BN / 16;                  // 1-KiB pieces per B stage
+  constexpr int IB = NB_TOT / NW;
+  static_assert(NB_TOT % NW == 0, "B pieces per wave");
+  constexpr int CS = BN + 4;
+  constexpr int EPI = NW * 16 * CS * 4;
+  constexpr int MAIN = 2 * HALO + 2 * B_STAGE;
+  constexpr int LDS_BYTES = MAIN > EPI ? MAIN : EPI;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
+  unsigned char* const halo0 = lds;
+  unsigned char* const ring = lds + 2 * HALO;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  int L = xcd_remap(blockIdx.x, p.nwg);
+  const int tile_n = L % p.tiles_n;
+  L /= p.tiles_n;
+  const int tw = L % tiles_w;
+  L /= tiles_w;
+  const int th = L % tiles_h;
+  const int n = L / tiles_h;
+  const int n0 = tile_n * BN;
+  const int oh0 = th * TR, ow0 = tw * TC;
+
+  // ---- halo DMA: piece q = pixels 8q .. 8q+7 (lane -> pixel 8q + lane/8, physical slot lane%8)
+  const float* xn = p.x + (int64_t)n * p.xsn;
+  auto halo_src = [&](int q, int c) -> const float* {
+    const int px = q * 8 + (lane >> 3);
+    const int hr = px / HW_, hc = px - hr * HW_;
+    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+    const int s = (lane & 7) ^ ((px >> 1) & 7);       // logical slot stored at this lane's slot
+    if (px >= HP || (unsigned)ih >= (unsigned)p.Hi || (unsigned)iw >= (unsigned)p.Wi) return p.zero;
+    return xn + (int64_t)ih * p.xsh + (int64_t)iw * p.xsw + c * HBK + s * 4;
+  };
+  auto issue_halo = [&](int q, int c, int buf) {
+    glds16(halo_src(q, c), halo0 + buf * HALO + q * 1024);
+  };
+
+  // ---- B pieces (as conv_wave.hip): piece j -> plane j / TN, rows 16 (j % TN) .. +16
+  const uint16_t* bsrc[IB];
+  int bdst[IB];
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int j = wave * IB + i;
+    const int q = j / (BN / 16), rb = j % (BN / 16);
+    const int nrow = rb * 16 + (lane >> 2);
+    const int ch = (lane & 3) ^ swzF(nrow);
+    const uint16_t* plane = F16 ? (q == 0 ? p.wh16 : p.wl16) : (q == 0 ? p.whi : p.wlo);
+    bsrc[i] = plane + (int64_t)(n0 + nrow) * p.k_pad + ch * 8;
+    bdst[i] = (q * BN + rb * 16) * 64;
+  }
+  auto issue_b = [&](int kt, int stage) {
+    unsigned char* sb = ring + stage * B_STAGE;
+#pragma unroll
+    for (int i = 0; i < IB; ++i) glds16(bsrc[i] + (int64_t)kt * HBK, sb + bdst[i]);
+  };
+
+  // precision 3: one frame per block -> one activation scale
+  float sa = 1.f, inv = 1.f;
+  if constexpr (F16) {
+    const int e = f16_scale_exp(p.x_amax[n]);
+    sa = ldexpf(1.f, 15 - e);
+    inv = ldexpf(1.f, e - 15);
+  }
+
+  // A fragment rows of this lane: row block rb = wave * TM + i -> tile row rb / (TC/16),
+  // pixels (rb % (TC/16)) * 16 + fr; halo pixel of tap (kh, kw) = base + kh * HW_ + kw
+  int hbase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rb = wave * TM + i;
+    hbase[i] = (rb / (TC / 16)) * HW_ + (rb % (TC / 16)) * 16 + fr;
+  }
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nc = p.Ci / HBK;
+  const int nk = nc * 9;
+  // prologue: the whole halo of chunk 0 and B(0)
+  for (int q = wave; q < HQ; q += NW) issue_halo(q, 0, 0);
+  issue_b(0, 0);
+
+  int kt = 0;
+  for (int c = 0; c < nc; ++c) {
+    const unsigned char* hb = halo0 + (c & 1) * HALO;
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t, ++kt) {
+      wait_barrier<0>();
+      if (kt + 1 < nk) issue_b(kt + 1, (kt + 1) & 1);
+      if (c + 1 < nc) {
+        const int q = t * NW + wave;                    // this wave's halo share of chunk c+1
+        if (q < HQ) issue_halo(q, c + 1, (c + 1) & 1);
+      }
+      const int kh = t / 3, kw = t - kh * 3;
+      // A fragments: 8 channels (two 16-B slots) of the tap-shifted pixel
+      frag_t af[NP][TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int px = hbase[i] + kh * HW_ + kw;
+        const int sw = (px >> 1) & 7;
+        const unsigned char* pp = hb + px * 128;
+        const f4 v0 = *reinterpret_cast<const f4*>(pp + (((2 * fg) ^ sw) << 4));
+        const f4 v1 = *reinterpret_cast<const f4*>(pp + (((2 * fg + 1) ^ sw) << 4));
+        if constexpr (APL) {
+          af[0][i] = __builtin_bit_cast(bf16x8, v0);
+          af[1][i] = __builtin_bit_cast(bf16x8, v1);
+        } else if constexpr (F16) {
+          unsigned long long p0[2], p1[2];
+          split_planes_f16(v0, sa, p0);
+          split_planes_f16(v1, sa, p1);
+#pragma unroll
+          for (int q = 0; q < 2; ++q) {
+            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+            af[q][i] = __builtin_bit_cast(f16x8, u64x2{p0[q], p1[q]});
+          }
+        } else {
+          bf16x4 p0[NP], p1[NP];
+          split_planes<NP>(v0, p0);
+          split_planes<NP>(v1, p1);
+#pragma unroll
+          for (int q = 0; q < NP; ++q)
+            af[q][i] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
+        }
+      }
+      const unsigned char* sb = ring + (kt & 1) * B_STAGE;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int nrow = j * 16 + fr;
+        const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
+        frag_t bfr[NP];
+#pragma unroll
+        for (int q = 0; q < NP; ++q) bfr[q] = *reinterpret_cast<const frag_t*>(bp + q * BN * 64);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int s = NP - 1; s >= 0; --s)
+#pragma unroll
+            for (int qa = s; qa >= 0; --qa) acc[i][j] = mfma16(af[qa][i], bfr[s - qa], acc[i][j]);
+      }
+    }
+  }
+  wait_barrier<0>();   // every DMA landed and every fragment read retired: LDS is free
+
+  // ---------------- epilogue: per-wave 16-row slices (one row block = 16 consecutive pixels)
+  float* ct = reinterpret_cast<float*>(lds) + wave * 16 * CS;
+  constexpr int CPR = BN / 4;
+  constexpr int RPP = 64 / CPR;
+  constexpr int EB = 16 / RPP;
+  const int cc = lane % CPR, rr0 = lane / CPR;
+  const int col = n0 + cc * 4;
+  const bool cval = col < p.Co;
+  f4 sc4 = {1.f, 1.f, 1.f, 1.f}, bi4 = {0.f, 0.f, 0.f, 0.f}, sl4 = {0.f, 0.f, 0.f, 0.f};
+  if (cval) {
+    if (p.scale) sc4 = *reinterpret_cast<const f4*>(p.scale + col);
+    if (p.bias) bi4 = *reinterpret_cast<const f4*>(p.bias + col);
+    if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
+  }
+  float ym = 0.f;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int rb = wave * TM + i;
+    const int oh = oh0 + rb / (TC / 16), owb = ow0 + (rb % (TC / 16)) * 16;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) ct[(fg * 4 + r) * CS + j * 16 + fr] = acc[i][j][r];
+    int64_t yo[EB];
+    f4 res[EB];
+    bool ok[EB];
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int ow = owb + rr0 + RPP * e;
+      ok[e] = cval && oh < p.Ho && ow < p.Wo;
+      res[e] = f4{0.f, 0.f, 0.f, 0.f};
+      yo[e] = 0;
+      if (ok[e]) {
+        yo[e] = (int64_t)n * p.ysn + (int64_t)oh * p.ysh + (int64_t)ow * p.ysw + col;
+        if (p.res_mode != PRPE_RES_NONE)
+          res[e] = *reinterpret_cast<const f4*>(p.r + (int64_t)n * p.rsn + (int64_t)oh * p.rsh + (int64_t)ow * p.rsw + col);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      f4 v = *reinterpret_cast<const f4*>(ct + (rr0 + RPP * e) * CS + cc * 4);
+      if (!ok[e]) continue;
+      if constexpr (F16) v = v * inv;
+      v = v * sc4 + bi4;
+      if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
+      if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
+      if (p.y_planes) {
+        bf16x4 pl[2];
+        split_planes<2>(v, pl);
+        uint16_t* y16 = reinterpret_cast<uint16_t*>(p.y) + 2 * (yo[e] - col) + (col >> 3) * 16 + (col & 7);
+        *reinterpret_cast<bf16x4*>(y16) = pl[0];
+        *reinterpret_cast<bf16x4*>(y16 + 8) = pl[1];
+      } else {
+        *reinterpret_cast<f4*>(p.y + yo[e]) = v;
+      }
+      if (p.y_amax) ym = fmaxf(ym, amax4(v));
+    }
+  }
+  if (p.y_amax) amax_commit(p.y_amax + n, ym);
+}
+
+template <int NW, int TR, int TC, int TN, bool F16, bool APL>
+int launch_halo(const ConvK& kp0, hipStream_t st) {
+  ConvK kp = kp0;
+  const int tiles_w = (kp.Wo + TC - 1) / TC, tiles_h = (kp.Ho + TR - 1) / TR;
+  kp.tiles_n = (kp.Co + TN * 16 - 1) / (TN * 16);
+  const int64_t nwg = (int64_t)(kp.M / kp.HoWo) * tiles_h * tiles_w * kp.tiles_n;
+  if (nwg <= 0 || nwg >= (1LL << 31)) return PRPE_EINVAL;
+  kp.nwg = (int)nwg;
+  hipLaunchKernelGGL((conv_halo_kernel<NW, TR, TC, TN, F16, APL>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp, tiles_w,
+                     tiles_h);
+  return launch_status();
+}
+
+template <int NW, int TR, int TC, int TN>
+int launch_halo_kind(const ConvK& kp, int prec, hipStream_t st) {
+  if (prec == 3) return launch_halo<NW, TR, TC, TN, true, false>(kp, st);
+  return kp.x_planes ? launch_halo<NW, TR, TC, TN, false, true>(kp, st) : launch_halo<NW, TR, TC, TN, false, false>(kp, st);
+}
+
+}  // namespace
+
+bool conv_halo_eligible(const ConvK& kp, int prec, int km) {
+  // 3x3 / stride 1 / pad 1 over whole 32-channel chunks (chunk-major weights), vectorised
+  // epilogue, precision 0 (fp32 or planes input) or 3 (fp16 planes + the input's max bound)
+  const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.x_planes;
+  return km == 2 && kp.KH == 3 && kp.KW == 3 && kp.stride == 1 && kp.pad == 1 && kp.Ci % HBK == 0 &&
+         kp.vec_out && (prec == 0 || p3) && !kp.in_scale && !kp.x2 && kp.k_pad == kp.K && kp.zero &&
+         kp.Hi == kp.Ho && kp.Wi == kp.Wo;
+}
+
+// Where the automatic choice takes it (measured in the model at bs = 256, r02_layer_profile_halo.txt):
+// the tile must cover the image with <= 5 % padding waste (10x10 and 40x40 trunk maps ran 1.1-1.9x
+// slower on 8 x 16 tiles), and an fp32-input precision-0 conv stays on the wave kernel (the
+// AdaFace adapter's 128->64 ran 8 % slower); planes input and precision 3 win (adapters' 3x3
+// 256->128 -3..-5 %, trunk layer1 3x3 -10 %).
+bool conv_halo_auto(const ConvK& kp, int prec) {
+  if (prec == 0 && !kp.x_planes) return false;
+  const int tc = 16, tr = 8;
+  const int64_t covered = (int64_t)((kp.Ho + tr - 1) / tr) * tr * ((kp.Wo + tc - 1) / tc) * tc;
+  return covered * 20 <= (int64_t)kp.Ho * kp.Wo * 21;
+}
+
+// tile 30 = auto: 8 x 16 output pixels, 4 waves (two workgroups per CU), 128 output channels
+// per workgroup, or 64 when Co <= 64 (tools/conv_bench.py, profiles/r02_conv_bench_halo.txt);
+// 31..35 force a configuration
+int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
+  if (tile == 30) tile = kp.Co <= 64 ? 34 : 31;
+  switch (tile) {
+    case 31: return launch_halo_kind<4, 8, 16, 8>(kp, prec, st);     // 8 x 16 px, 4 waves, 128 ch
+    case 32: return launch_halo_kind<8, 16, 16, 8>(kp, prec, st);    // 16 x 16 px, 8 waves, 128 ch
+    case 33: return launch_halo_kind<8, 8, 32, 8>(kp, prec, st);     // 8 x 32 px, 8 waves, 128 ch
+    case 34: return launch_halo_kind<4, 8, 16, 4>(kp, prec, st);     // 8 x 16 px, 4 waves, 64 ch
+    case 35: return launch_halo_kind<8, 16, 16, 4>(kp, prec, st);    // 16 x 16 px, 8 waves, 64 ch
+    default: return PRPE_EINVAL;
+  }
+}
+
+}  // namespace prpe_k

@@ -679,6 +679,17 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const char* e = getenv("PRPE_CONV_WAVE");
     return e && e[0] == '0' ? 0 : 1;
   }();
+  // haloed-tile 3x3 kernel (conv_halo.hip): the automatic choice for the 3x3 / s1 / p1 convs
+  // where conv_halo_auto says it wins (profiles/r02_conv_bench_halo.txt, in-model per-layer
+  // profile r02_layer_profile_halo.txt); tiles 30..35 force it, PRPE_CONV_HALO=0 turns it off
+  static const int halo_on = [] {
+    const char* e = getenv("PRPE_CONV_HALO");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  if (tile >= 30 && tile < 40)
+    return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;
+  if (tile == 0 && halo_on && conv_halo_auto(kp, prec) && conv_halo_eligible(kp, prec, km))
+    return conv_halo_launch(kp, prec, 30, st);
   // precision 3 (split fp16) is implemented by the wave-row kernel only
   if (prec == 3) {
     if (tile != 0 && tile < 20) return PRPE_EINVAL;

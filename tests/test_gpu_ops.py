@@ -304,6 +304,52 @@ def test_conv_f16_two_stage_ring_bit_exact(B, Ci, H, W, Co, k, s, p):
     assert torch.equal(a, b) and ya == yb
 
 
+HALO_SHAPES = [
+    (2, 64, 17, 19, 96, 3, 1, 1),       # ragged in both spatial dims (partial tiles), Co < 128
+    (3, 96, 13, 17, 136, 3, 1, 1),      # Co beyond one 128 tile, odd chunk count
+    (1, 256, 33, 40, 128, 3, 1, 1),     # 8 chunks (halo double buffer wraps 4 times)
+    (2, 32, 16, 16, 256, 3, 1, 1),      # one chunk (no halo prefetch), two Co tiles, exact tiles
+]
+
+
+@pytest.mark.parametrize("tile", [30, 31, 32, 33, 34, 35])
+@pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", HALO_SHAPES)
+def test_conv_halo_kernel_bit_exact_vs_wave(B, Ci, H, W, Co, k, s, p, tile):
+    """conv_halo.hip (input patch + halo staged once per 32-channel chunk, A fragments of every
+    tap from LDS) runs the wave kernel's K order, split and MFMA order: bit-identical to it,
+    with a pre-activation residual and GELU, for fp32 input, planes input and precision 3."""
+    x = rnd(B, Ci, H, W, seed=180)
+    w = rnd(Co, Ci, k, k, seed=181, scale=1.0 / math.sqrt(Ci * k * k))
+    sc = torch.rand(Co, generator=_g(182)) + 0.5
+    bi = rnd(Co, seed=183)
+    r = rnd(B, Co, H, W, seed=184)
+    kw = dict(act="gelu", scale=sc, bias=bi, k_order=1, precision=0, res=r, res_mode=RES_PRE)
+    got = run_conv(x, w, s, p, tile=tile, **kw)
+    assert torch.equal(got, run_conv(x, w, s, p, tile=28, **kw))
+    ref = ref_conv(x, w, s, p, act="gelu", scale=sc, bias=bi, res=r, res_mode=RES_PRE)
+    torch.testing.assert_close(got, ref, rtol=0, atol=_tol(x, w) * 2)
+    # planes input (the adapters' upconv output format) and planes output
+    pk = pack.pack_conv("h", w, 1, 1, DEV, scale=sc, bias=bi, act="gelu", k_order=1)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    xpl = torch.empty_like(xd)
+    ops.conv2d(xd, pack.pack_conv("i", torch.eye(Ci).view(Ci, Ci, 1, 1), 1, 0, DEV), xpl, precision=2,
+               y_planes=True)
+    outs = []
+    for t in (tile, 28):
+        y = torch.empty(B, H, W, Co, device=DEV)
+        ops.conv2d(xpl, pk, y, precision=0, x_planes=True, tile=t)
+        ypl = torch.empty(B, H, W, Co, device=DEV)
+        ops.conv2d(xd, pk, ypl, precision=0, y_planes=True, tile=t)
+        outs.append((y, ypl))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    # precision 3 with per-frame scales and max|y| slots
+    xp = torch.relu(x) * 7.0
+    a, ya = _conv_p3(xp, w, s, p, tile=tile, scale=sc, bias=bi, act="silu")
+    b, yb = _conv_p3(xp, w, s, p, tile=27, scale=sc, bias=bi, act="silu")
+    assert torch.equal(a, b) and ya == yb
+
+
 @pytest.mark.parametrize("mode", [RES_PRE, RES_POST])
 @pytest.mark.parametrize("tile", [21, 23])
 def test_conv_wave_kernel_prologue_residual_prelu(mode, tile):
