@@ -166,11 +166,13 @@ int prpe_upsample_nearest2x(const prpe_view* x, const prpe_view* y, void* stream
  * y = sigmoid((x - mean_hw) / (std_hw_unbiased + 1e-6)). */
 int prpe_norm_sigmoid(const prpe_view* x, const prpe_view* y, void* stream);
 
-/* LayerNorm over the last dim of rows (ViTPose, eps 1e-12), optional ReLU on the output
- * (simple decoder's ReLU, modeling_vitpose.py:139). x/y: [rows][C] with row strides. */
+/* LayerNorm over the last dim of rows (ViTPose, eps 1e-12). x/y: [rows][C] with row strides.
+ * flags: bit 0 = ReLU on the output (simple decoder's ReLU, modeling_vitpose.py:139); bit 1 =
+ * write y in the planes format described at prpe_conv_desc: C % 8 == 0, C <= 1024, 16-B aligned x rows,
+ * 32-B aligned y rows; the input format of the precision-0 GEMM that consumes it. */
 int prpe_layernorm(const float* x, int64_t x_row_stride, float* y, int64_t y_row_stride,
                    int64_t rows, int32_t C, const float* gamma, const float* beta,
-                   float eps, int32_t relu, void* stream);
+                   float eps, int32_t flags, void* stream);
 
 /* ViT multi-head self-attention, softmax(Q K^T * scale) V per (frame, head).
  * qkv: [B*L][3*H*D] rows (q | k | v, head-major inside each), out: [B*L][H*D].
@@ -183,10 +185,11 @@ int prpe_attention(const float* qkv, float* out, int32_t B, int32_t L, int32_t H
  * strides multiples of 4 elements, qkv 16-B aligned. prpe_attention is the row-major case
  * (s_frame = L*3*H*D, s_which = H*D, s_head = D, s_tok = 3*H*D); a head-major QKV GEMM output
  * [B][3][H][L][D] (s_frame = 3*H*L*D, s_which = H*L*D, s_head = L*D, s_tok = D) gives every
- * head's K and V as one contiguous 48-KB block. out: [B*L][H*D]. */
+ * head's K and V as one contiguous 48-KB block. out: [B*L][H*D], in the planes format of
+ * prpe_conv_desc when out_planes != 0 (the input format of the precision-0 projection GEMM). */
 int prpe_attention_strided(const float* qkv, int64_t s_frame, int64_t s_which, int64_t s_head,
                            int64_t s_tok, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
-                           float scale, void* stream);
+                           float scale, int32_t out_planes, void* stream);
 
 /* YOLO PSA attention core (nn.py:111-122): per frame, per head:
  *   out[c, i] = sum_j v[c, j] softmax_j(q[:, i] . k[:, j] * scale)

@@ -365,7 +365,7 @@ struct AttnStrides {
   int64_t frame, which, head, tok;
 };
 
-template <int KC>
+template <int KC, bool OPL>
 __global__ __launch_bounds__(NWAVE * 64) void vit_attention_s_kernel(const float* __restrict__ qkv, AttnStrides sd,
                                                                     float* __restrict__ out, int H, int hpw,
                                                                     float scale) {
@@ -552,9 +552,13 @@ __global__ __launch_bounds__(NWAVE * 64) void vit_attention_s_kernel(const float
     }
     if (c == NCH - 1) {
       const float inv = __builtin_amdgcn_rcpf(l);
-      float* orow = out + ((int64_t)b * AL + q0 + fr) * HD + (h0 + it / NCH) * AD + fg * 4;
+      float* prow = out + ((int64_t)b * AL + q0 + fr) * HD;
+      const int c0 = (h0 + it / NCH) * AD + fg * 4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) *reinterpret_cast<f32x4*>(orow + j * 16) = o[j] * inv;
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (OPL) store_planes4(reinterpret_cast<uint16_t*>(prow), c0 + j * 16, o[j] * inv);
+        else *reinterpret_cast<f32x4*>(prow + c0 + j * 16) = o[j] * inv;
+      }
     }
   }
 }
@@ -601,7 +605,7 @@ __global__ __launch_bounds__(256) void psa_attention_kernel(prpe_view qkv, prpe_
 }
 
 int attention_launch(const float* qkv, AttnStrides sd, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
-                            float scale, void* stream) {
+                     float scale, int out_planes, void* stream) {
   if (!qkv || !out || B <= 0 || H <= 0 || L != AL || D != AD) return PRPE_EINVAL;
   if ((uintptr_t)qkv % 16 || (uintptr_t)out % 16) return PRPE_EINVAL;
   if (sd.frame % 4 || sd.which % 4 || sd.head % 4 || sd.tok % 4) return PRPE_EINVAL;
@@ -622,15 +626,20 @@ int attention_launch(const float* qkv, AttnStrides sd, float* out, int32_t B, in
   int hpw = H;
   while (hpw > 1 && ((int64_t)B * H / hpw < 256 || H % hpw)) --hpw;
   const dim3 gs(B * H / hpw);
+  if (out_planes) {
+    if ((uintptr_t)out % 32) return PRPE_EINVAL;
+    hipLaunchKernelGGL((vit_attention_s_kernel<64, true>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale);
+    return launch_status();
+  }
   switch (rowmajor ? sel : 64) {
     case 1: hipLaunchKernelGGL(vit_attention_kernel, g, dim3(NWAVE * 64), 0, st, qkv, out, H, scale); break;
     case 322: hipLaunchKernelGGL((vit_attention_t_kernel<32, 2>), g, dim3(6 * 64), 0, st, qkv, out, H, scale); break;
     case 641: hipLaunchKernelGGL((vit_attention_t_kernel<64, 1>), g, dim3(12 * 64), 0, st, qkv, out, H, scale); break;
     case 642: hipLaunchKernelGGL((vit_attention_t_kernel<64, 2>), g, dim3(6 * 64), 0, st, qkv, out, H, scale); break;
     case 962: hipLaunchKernelGGL((vit_attention_t_kernel<96, 2>), g, dim3(6 * 64), 0, st, qkv, out, H, scale); break;
-    case 32: hipLaunchKernelGGL(vit_attention_s_kernel<32>, gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale); break;
-    case 96: hipLaunchKernelGGL(vit_attention_s_kernel<96>, gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale); break;
-    default: hipLaunchKernelGGL(vit_attention_s_kernel<64>, gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale); break;
+    case 32: hipLaunchKernelGGL((vit_attention_s_kernel<32, false>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale); break;
+    case 96: hipLaunchKernelGGL((vit_attention_s_kernel<96, false>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale); break;
+    default: hipLaunchKernelGGL((vit_attention_s_kernel<64, false>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale); break;
   }
   return launch_status();
 }
@@ -640,13 +649,14 @@ int attention_launch(const float* qkv, AttnStrides sd, float* out, int32_t B, in
 extern "C" int prpe_attention(const float* qkv, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
                               float scale, void* stream) {
   const int64_t HD = (int64_t)H * D;
-  return attention_launch(qkv, AttnStrides{(int64_t)L * 3 * HD, HD, D, 3 * HD}, out, B, L, H, D, scale, stream);
+  return attention_launch(qkv, AttnStrides{(int64_t)L * 3 * HD, HD, D, 3 * HD}, out, B, L, H, D, scale, 0, stream);
 }
 
 extern "C" int prpe_attention_strided(const float* qkv, int64_t s_frame, int64_t s_which, int64_t s_head,
                                       int64_t s_tok, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
-                                      float scale, void* stream) {
-  return attention_launch(qkv, AttnStrides{s_frame, s_which, s_head, s_tok}, out, B, L, H, D, scale, stream);
+                                      float scale, int32_t out_planes, void* stream) {
+  return attention_launch(qkv, AttnStrides{s_frame, s_which, s_head, s_tok}, out, B, L, H, D, scale, out_planes,
+                          stream);
 }
 
 extern "C" int prpe_psa_attention(const prpe_view* qkv, const prpe_view* out, const prpe_view* vout, int32_t nh,

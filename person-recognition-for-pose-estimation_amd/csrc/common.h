@@ -52,6 +52,27 @@ __device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {
   lo = (__bf16)(x - (float)hi);
 }
 
+// 4 consecutive channels c .. c+3 (c % 4 == 0) of one pixel in the planes format (prpe.h,
+// prpe_conv_desc): channel group c / 8 holds hi[8] then lo[8], hi = RNE(v), lo = RNE(v - hi).
+// row16: the pixel's first bf16 slot. The remainder is an explicit v_sub_f32: with FP
+// contraction the compiler would fuse a producing multiply into it (fma(a, b, -hi)) and the
+// planes would no longer be the split of the stored fp32 value.
+__device__ __forceinline__ void store_planes4(uint16_t* row16, int c, f32x4 v) {
+  uint16_t* y16 = row16 + (c >> 3) * 16 + (c & 7);
+  unsigned short hi[4], lo[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float x = v[e];
+    const __bf16 h = (__bf16)x;
+    float d;
+    asm("v_sub_f32 %0, %1, %2" : "=v"(d) : "v"(x), "v"((float)h));
+    hi[e] = __builtin_bit_cast(unsigned short, h);
+    lo[e] = __builtin_bit_cast(unsigned short, (__bf16)d);
+  }
+  *reinterpret_cast<uint2*>(y16) = make_uint2(hi[0] | (unsigned)hi[1] << 16, hi[2] | (unsigned)hi[3] << 16);
+  *reinterpret_cast<uint2*>(y16 + 8) = make_uint2(lo[0] | (unsigned)lo[1] << 16, lo[2] | (unsigned)lo[3] << 16);
+}
+
 __device__ __forceinline__ float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

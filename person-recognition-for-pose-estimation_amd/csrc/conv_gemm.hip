@@ -1,0 +1,242 @@
+// 1x1 convolutions / linears (a plain GEMM over contiguous pixels: M = pixels, K = Ci,
+// N = Co) on 256-row block tiles with BOTH operands staged in LDS by LDS-DMA.
+//
+// Why (tools/conv_bench.py ablations, profiles/r02_conv_ablation.txt): in the wave-row kernel a
+// 128 x 128 block issues 8 vector-memory instructions per wave for every 48 MFMAs (A fragment
+// loads + B ring DMA), and removing them makes the ViT fc2 GEMM 2x faster. A 256 x 256 tile
+// halves the memory instructions per MFMA: per 32-deep K-step the block DMAs 32 KB of A (256
+// rows x 32 channels, full 128-B lines) and 32 KB of B (2 planes x 256 columns x 64 B) -- 8
+// pieces per wave -- for 96 MFMAs per wave; each A row is read from LDS by the 4 waves that
+// share it instead of being fetched from L2 by one wave per column tile.
+// Measured (profiles/r02_conv_bench_gemm.txt): that 256 x 256 two-stage tile (41) exposes the
+// DMA latency (one block per CU, one step of lookahead) and loses to a 256 x 128 tile with a
+// three-stage ring (40, the automatic one: 8 waves = 4 (M) x 2 (N), wave tile 64 x 64,
+// 6 pieces per wave for 48 MFMAs, 144 KB LDS, two steps of lookahead).
+//
+// Per K-step: counted vmcnt + s_barrier (step kt landed, step kt+1 may be in flight), then the
+// DMA of step kt + STAGES - 1 into the stage read at kt - 1 (pieces spread over this step's
+// row blocks), fragments of step kt from LDS, MFMAs. Same K order, plane split and
+// per-accumulator MFMA order as conv_wave.hip (bit-identical results, tested).
+//
+// LDS per stage: A [256 rows][8 slots x 16 B] (slot s of row r at s ^ ((r >> 1) & 7):
+// conflict-free ds_read_b128 of 16 consecutive rows) then B [2 planes][BN cols][64 B]
+// (conv_wave's swizzle). The epilogue slab reuses stage 0.
+#include "conv.h"
+
+namespace prpe_k {
+namespace {
+
+constexpr int GBK = 32;
+
+template <int BN, int WM, int STAGES, bool APL>
+__global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
+  constexpr int NW = 8, BM = 256, NP = 2;
+  constexpr int WN = NW / WM;                          // waves along N
+  constexpr int WTN = BN / WN;                         // wave tile (BM / WM) x WTN
+  constexpr int TM = BM / WM / 16, TN = WTN / 16;
+  constexpr int A_BYTES = BM * 128;                    // 32 KB
+  constexpr int B_BYTES = NP * BN * 64;
+  constexpr int STAGE = A_BYTES + B_BYTES;
+  constexpr int NA = A_BYTES / 1024, NBP = B_BYTES / 1024;
+  constexpr int PW = (NA + NBP) / NW;                  // pieces per wave and K-step
+  static_assert((NA + NBP) % NW == 0, "pieces");
+  constexpr int CS = WTN + 4;                          // epilogue row pitch (floats)
+  static_assert(NW * 16 * CS * 4 <= STAGE, "epilogue slab");
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[STAGES * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int wm = wave / WN, wn = wave % WN;
+  const int L = xcd_remap(blockIdx.x, p.nwg);
+  const int tile_m = L / p.tiles_n, tile_n = L % p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  // ---- this wave's DMA pieces: j = wave * PW + i; j < NA: A rows 8j .. 8j+7, else B
+  const float* src[PW];
+  int dst[PW];
+#pragma unroll
+  for (int i = 0; i < PW; ++i) {
+    const int j = wave * PW + i;
+    if (j < NA) {
+      const int row = j * 8 + (lane >> 3);
+      const int s = (lane & 7) ^ ((row >> 1) & 7);     // logical slot landing in this lane's slot
+      const int m = m0 + row < p.M ? m0 + row : p.M - 1;   // tail rows re-read the last row
+      src[i] = p.x + (int64_t)m * p.xsw + s * 4;
+      dst[i] = j * 1024;
+    } else {
+      const int jb = j - NA;
+      const int q = jb / (BN / 16), rb = jb % (BN / 16);
+      const int nrow = rb * 16 + (lane >> 2);
+      const int ch = (lane & 3) ^ swzF(nrow);
+      const uint16_t* plane = q == 0 ? p.whi : p.wlo;
+      src[i] = reinterpret_cast<const float*>(plane + (int64_t)(n0 + nrow) * p.k_pad + ch * 8);
+      dst[i] = A_BYTES + (q * BN + rb * 16) * 64;
+    }
+  }
+  // K-step advance of each piece's source: A 32 channels (floats), B 32 bf16 = 16 floats
+  auto piece = [&](int i, int kt, int stage) {
+    const int j = wave * PW + i;
+    const float* s = src[i] + (int64_t)kt * (j < NA ? GBK : GBK / 2);
+    glds16(s, lds + stage * STAGE + dst[i]);
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = p.nk;
+#pragma unroll
+  for (int i = 0; i < PW; ++i) piece(i, 0, 0);
+  if constexpr (STAGES == 3) {
+#pragma unroll
+    for (int i = 0; i < PW; ++i) piece(i, nk > 1 ? 1 : 0, 1);
+  }
+
+  int st = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // step kt landed (with 3 stages the PW pieces of step kt+1 may stay in flight)
+    wait_barrier<(STAGES - 2) * PW>();
+    // the step issued now (kt + STAGES - 1, clamped to the last: a harmless re-read into the
+    // stage read at kt - 1, so the wait counts stay exact) goes into that stage
+    const int ks = kt + STAGES - 1 < nk ? kt + STAGES - 1 : nk - 1;
+    const int sn = st == 0 ? STAGES - 1 : st - 1;
+    const bool more = STAGES == 3 || kt + 1 < nk;
+    const unsigned char* sa = lds + st * STAGE;
+    const unsigned char* sb = sa + A_BYTES;
+    // B fragments of the wave's 4 column blocks (both planes), held for the whole step
+    bf16x8 bfr[TN][NP];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int nrow = wn * WTN + j * 16 + fr;
+      const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
+#pragma unroll
+      for (int q = 0; q < NP; ++q) bfr[j][q] = *reinterpret_cast<const bf16x8*>(bp + q * BN * 64);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      if (more) {                                       // the DMA pieces spread over the row blocks
+#pragma unroll
+        for (int u = PW * i / TM; u < PW * (i + 1) / TM; ++u) piece(u, ks, sn);
+      }
+      const int row = wm * (BM / WM) + i * 16 + fr;
+      const int sw = (row >> 1) & 7;
+      const unsigned char* ap = sa + row * 128;
+      const f4 v0 = *reinterpret_cast<const f4*>(ap + (((2 * fg) ^ sw) << 4));
+      const f4 v1 = *reinterpret_cast<const f4*>(ap + (((2 * fg + 1) ^ sw) << 4));
+      bf16x8 af[NP];
+      if constexpr (APL) {
+        af[0] = __builtin_bit_cast(bf16x8, v0);
+        af[1] = __builtin_bit_cast(bf16x8, v1);
+      } else {
+        bf16x4 p0[NP], p1[NP];
+        split_planes<NP>(v0, p0);
+        split_planes<NP>(v1, p1);
+#pragma unroll
+        for (int q = 0; q < NP; ++q)
+          af[q] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int s = NP - 1; s >= 0; --s)
+#pragma unroll
+          for (int qa = s; qa >= 0; --qa) acc[i][j] = mfma16(af[qa], bfr[j][s - qa], acc[i][j]);
+    }
+    st = st + 1 == STAGES ? 0 : st + 1;
+  }
+  wait_barrier<0>();
+
+  // ---------------- epilogue: per-wave 16-row x 64-column slices, 16-B row stores
+  float* ct = reinterpret_cast<float*>(lds) + wave * 16 * CS;
+  constexpr int CPR = WTN / 4, RPP = 64 / CPR, EB = 16 / RPP;
+  const int cc = lane % CPR, rr0 = lane / CPR;
+  const int col = n0 + wn * WTN + cc * 4;
+  const bool cval = col < p.Co;
+  f4 sc4 = {1.f, 1.f, 1.f, 1.f}, bi4 = {0.f, 0.f, 0.f, 0.f}, sl4 = {0.f, 0.f, 0.f, 0.f};
+  if (cval) {
+    if (p.scale) sc4 = *reinterpret_cast<const f4*>(p.scale + col);
+    if (p.bias) bi4 = *reinterpret_cast<const f4*>(p.bias + col);
+    if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
+  }
+  FrameMax ymax;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) ct[(fg * 4 + r) * CS + j * 16 + fr] = acc[i][j][r];
+    __builtin_amdgcn_wave_barrier();
+    f4 res[EB];
+    bool ok[EB];
+    int mm[EB];
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      const int m = m0 + wm * (BM / WM) + i * 16 + rr0 + RPP * e;
+      mm[e] = m;
+      ok[e] = cval && m < p.M;
+      res[e] = f4{0.f, 0.f, 0.f, 0.f};
+      if (ok[e] && p.res_mode != PRPE_RES_NONE) res[e] = *reinterpret_cast<const f4*>(p.r + (int64_t)m * p.rsw + col);
+    }
+#pragma unroll
+    for (int e = 0; e < EB; ++e) {
+      f4 v = *reinterpret_cast<const f4*>(ct + (rr0 + RPP * e) * CS + cc * 4);
+      if (!ok[e]) continue;
+      v = v * sc4 + bi4;
+      if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
+      if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
+      const int64_t yo = (int64_t)mm[e] * p.ysw + col;
+      if (p.y_planes) {
+        bf16x4 pl[2];
+        split_planes<2>(v, pl);
+        uint16_t* y16 = reinterpret_cast<uint16_t*>(p.y) + 2 * (yo - col) + (col >> 3) * 16 + (col & 7);
+        *reinterpret_cast<bf16x4*>(y16) = pl[0];
+        *reinterpret_cast<bf16x4*>(y16 + 8) = pl[1];
+      } else {
+        *reinterpret_cast<f4*>(p.y + yo) = v;
+      }
+      if (p.y_amax) ymax.add(p.y_amax, mm[e] / p.HoWo, amax4(v));
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (p.y_amax) frame_amax_final(p.y_amax, ymax);
+}
+
+}  // namespace
+
+bool conv_gemm_eligible(const ConvK& kp, int prec) {
+  // 1x1 / stride 1 / pad 0 over contiguous pixels (x, y, residual rows at one pixel stride),
+  // whole 32-channel K-steps, Co a multiple of 128, precision 0 (fp32 or planes input),
+  // vectorised epilogue, no prologue / dual input
+  const bool xlin = kp.xsh == (int64_t)kp.Wi * kp.xsw && kp.xsn == (int64_t)kp.Hi * kp.xsh && kp.xsc == 1;
+  return prec == 0 && kp.KH == 1 && kp.KW == 1 && kp.stride == 1 && kp.pad == 0 && kp.Ci % GBK == 0 &&
+         kp.K == kp.Ci && kp.k_pad == kp.K && kp.Co % 128 == 0 && kp.vec_out && kp.ylin && kp.rlin && xlin &&
+         !kp.in_scale && !kp.x2 && kp.xsw % 4 == 0 && kp.whi && kp.wlo;
+}
+
+template <int BN, int WM, int STAGES>
+int launch_gemm(const ConvK& kp0, hipStream_t st) {
+  if (kp0.Co % BN) return PRPE_EINVAL;
+  ConvK kp = kp0;
+  kp.tiles_n = kp.Co / BN;
+  const int64_t nwg = (int64_t)((kp.M + 255) / 256) * kp.tiles_n;
+  if (nwg >= (1LL << 31)) return PRPE_EINVAL;
+  kp.nwg = (int)nwg;
+  if (kp.x_planes) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, true>), dim3(kp.nwg), dim3(512), 0, st, kp);
+  else hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false>), dim3(kp.nwg), dim3(512), 0, st, kp);
+  return launch_status();
+}
+
+// tile 40 = auto (256 x 128, 3 stages), 41 = 256 x 256 (2 stages), 42 = 256 x 128 (2 stages)
+int conv_gemm_launch(const ConvK& kp, int tile, hipStream_t st) {
+  switch (tile) {
+    case 41: return launch_gemm<256, 2, 2>(kp, st);
+    case 42: return launch_gemm<128, 4, 2>(kp, st);
+    default: return launch_gemm<128, 4, 3>(kp, st);
+  }
+}
+
+}  // namespace prpe_k

@@ -686,6 +686,17 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const char* e = getenv("PRPE_CONV_HALO");
     return e && e[0] == '0' ? 0 : 1;
   }();
+  // 256-row GEMM kernel (conv_gemm.hip): the automatic choice for eligible 1x1 convs / linears
+  // over at least 32K pixels whose input is in the planes format (in the model: ViT fc2 -16 %,
+  // YOLO adapter 1x1 -9 %; with fp32 input it measured no better than the wave kernel there,
+  // profiles/r02_layer_profile_gemm_ab.txt); tiles 40..42 force it, PRPE_CONV_GEMM=0 turns it off
+  static const int gemm_on = [] {
+    const char* e = getenv("PRPE_CONV_GEMM");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
+  if (tile >= 40 && tile < 50) return conv_gemm_eligible(kp, prec) ? conv_gemm_launch(kp, tile, st) : PRPE_EINVAL;
+  if (tile == 0 && gemm_on && kp.x_planes && kp.M >= (1 << 15) && conv_gemm_eligible(kp, prec))
+    return conv_gemm_launch(kp, 40, st);
   if (tile >= 30 && tile < 40)
     return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;
   if (tile == 0 && halo_on && conv_halo_auto(kp, prec) && conv_halo_eligible(kp, prec, km))

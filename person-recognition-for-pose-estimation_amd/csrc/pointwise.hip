@@ -524,11 +524,12 @@ __global__ __launch_bounds__(256) void layernorm_reg_kernel(const float* __restr
     if (c < C) {
       const f4v gg = *reinterpret_cast<const f4v*>(g + c), bb = *reinterpret_cast<const f4v*>(b + c);
       f4v o = (v[i] - mean) * rstd * gg + bb;
-      if (relu) {
+      if (relu & 1) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = o[e] > 0.f ? o[e] : 0.f;
       }
-      *reinterpret_cast<f4v*>(yr + c) = o;
+      if (relu & 2) store_planes4(reinterpret_cast<uint16_t*>(yr), c, o);
+      else *reinterpret_cast<f4v*>(yr + c) = o;
     }
   }
 }
@@ -788,10 +789,14 @@ extern "C" int prpe_norm_sigmoid(const prpe_view* x, const prpe_view* y, void* s
 }
 
 extern "C" int prpe_layernorm(const float* x, int64_t xs, float* y, int64_t ys, int64_t rows, int32_t C,
-                              const float* g, const float* b, float eps, int32_t relu, void* stream) {
+                              const float* g, const float* b, float eps, int32_t flags, void* stream) {
   if (!x || !y || !g || !b || rows <= 0 || C <= 0) return PRPE_EINVAL;
+  if (flags & ~3) return PRPE_EINVAL;
   const bool al = C % 4 == 0 && xs % 4 == 0 && ys % 4 == 0 && (uintptr_t)x % 16 == 0 && (uintptr_t)y % 16 == 0 &&
                   (uintptr_t)g % 16 == 0 && (uintptr_t)b % 16 == 0;
+  // planes output (flags bit 1): the register-resident kernels only, whole 8-channel groups
+  if ((flags & 2) && (!al || C % 8 || C > 1024 || ys % 8 || (uintptr_t)y % 32)) return PRPE_EINVAL;
+  const int relu = flags;
   const dim3 grid((unsigned)((rows + 3) / 4));
   hipStream_t st = as_stream(stream);
   if (al && C <= 256) { hipLaunchKernelGGL(layernorm_reg_kernel<1>, grid, dim3(256), 0, st, x, xs, y, ys, rows, C, g, b, eps, relu); return launch_status(); }
@@ -799,7 +804,7 @@ extern "C" int prpe_layernorm(const float* x, int64_t xs, float* y, int64_t ys, 
   if (al && C <= 768) { hipLaunchKernelGGL(layernorm_reg_kernel<3>, grid, dim3(256), 0, st, x, xs, y, ys, rows, C, g, b, eps, relu); return launch_status(); }
   if (al && C <= 1024) { hipLaunchKernelGGL(layernorm_reg_kernel<4>, grid, dim3(256), 0, st, x, xs, y, ys, rows, C, g, b, eps, relu); return launch_status(); }
   hipLaunchKernelGGL(layernorm_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, as_stream(stream), x, xs, y,
-                     ys, rows, C, g, b, eps, relu);
+                     ys, rows, C, g, b, eps, relu & 1);
   return launch_status();
 }
 

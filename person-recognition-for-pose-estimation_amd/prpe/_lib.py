@@ -58,7 +58,7 @@ SIGNATURES = {
     "prpe_norm_sigmoid": (C.c_int, [_VP, _VP, _P]),
     "prpe_layernorm": (C.c_int, [_P, _L, _P, _L, _L, _I, _P, _P, _F, _I, _P]),
     "prpe_attention": (C.c_int, [_P, _P, _I, _I, _I, _I, _F, _P]),
-    "prpe_attention_strided": (C.c_int, [_P, _L, _L, _L, _L, _P, _I, _I, _I, _I, _F, _P]),
+    "prpe_attention_strided": (C.c_int, [_P, _L, _L, _L, _L, _P, _I, _I, _I, _I, _F, _I, _P]),
     "prpe_psa_attention": (C.c_int, [_VP, _VP, _VP, _I, _I, _I, _F, _P]),
     "prpe_dfl_decode": (C.c_int, [_P, _P, _I, _I, _I, C.POINTER(C.c_int32), C.POINTER(C.c_float), _P]),
     "prpe_l2norm": (C.c_int, [_P, _P, _P, _I, _I, C.c_float, _P]),

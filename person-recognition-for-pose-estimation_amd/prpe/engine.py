@@ -525,21 +525,31 @@ class Engine:
         self.conv(pix, patch, out=X, res=pos_v, res_mode=RES_PRE)
         X2 = X.view(B * L, D)
         as4 = lambda t: t.view(t.shape[0], 1, 1, t.shape[1])
+
+        def as4p(t):
+            # the producer wrote the planes format: the GEMM consumer reads it without a split
+            t4 = as4(t)
+            t4._prpe_planes = pl
+            return t4
+        # LayerNorm and attention write their outputs in the planes format when precision 0
+        # consumes them (qkv / fc1 / proj GEMMs: the operand split done once by the producer)
+        pl = PLANES_ON and self.precision == 0
+        Hh, Dh = arch.VIT_HEADS, D // arch.VIT_HEADS
         for i in range(arch.VIT_LAYERS):
             q = f"{v}.encoder.layer.{i}"
             A = q + ".attention.attention"
             hn = ops.layernorm(X2, self.empty(B * L, D), self.dev(q + ".layernorm_before.weight"),
-                               self.dev(q + ".layernorm_before.bias"))
-            qkv = self.conv(as4(hn), self._lin(q + ":qkv", [A + ".query.weight", A + ".key.weight", A + ".value.weight"],
-                                               [A + ".query.bias", A + ".key.bias", A + ".value.bias"]))
-            ctx = ops.attention(qkv.view(B * L, 3 * D), self.empty(B * L, D), B, L, arch.VIT_HEADS,
-                                D // arch.VIT_HEADS, (D // arch.VIT_HEADS) ** -0.5)
-            X2 = self.conv(as4(ctx), self._lin(q + ":proj", q + ".attention.output.dense.weight",
-                                               q + ".attention.output.dense.bias"),
+                               self.dev(q + ".layernorm_before.bias"), planes=pl)
+            qkv = self.conv(as4p(hn), self._lin(q + ":qkv", [A + ".query.weight", A + ".key.weight", A + ".value.weight"],
+                                                [A + ".query.bias", A + ".key.bias", A + ".value.bias"]))
+            ctx = ops.attention_strided(qkv, (L * 3 * D, D, Dh, 3 * D), self.empty(B * L, D), B, L, Hh, Dh,
+                                        Dh ** -0.5, out_planes=pl)
+            X2 = self.conv(as4p(ctx), self._lin(q + ":proj", q + ".attention.output.dense.weight",
+                                                q + ".attention.output.dense.bias"),
                            res=as4(X2), res_mode=RES_PRE).view(B * L, D)
             hn = ops.layernorm(X2, self.empty(B * L, D), self.dev(q + ".layernorm_after.weight"),
-                               self.dev(q + ".layernorm_after.bias"))
-            f1 = self.conv(as4(hn), self._lin(q + ":fc1", q + ".mlp.fc1.weight", q + ".mlp.fc1.bias", act="gelu"),
+                               self.dev(q + ".layernorm_after.bias"), planes=pl)
+            f1 = self.conv(as4p(hn), self._lin(q + ":fc1", q + ".mlp.fc1.weight", q + ".mlp.fc1.bias", act="gelu"),
                            planes_out=True)
             X2 = self.conv(f1, self._lin(q + ":fc2", q + ".mlp.fc2.weight", q + ".mlp.fc2.bias"),
                            res=as4(X2), res_mode=RES_PRE).view(B * L, D)

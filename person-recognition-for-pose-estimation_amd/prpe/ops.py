@@ -131,12 +131,13 @@ def norm_sigmoid(x, y):
     return y
 
 
-def layernorm(x2d, y2d, gamma, beta, eps=1e-12, relu=False):
+def layernorm(x2d, y2d, gamma, beta, eps=1e-12, relu=False, planes=False):
+    """planes: write y2d in the planes format (prpe.h) for a precision-0 GEMM consumer."""
     _gpu(x2d, y2d, gamma, beta)
     rows, c = x2d.shape
     check(lib().prpe_layernorm(x2d.data_ptr(), x2d.stride(0), y2d.data_ptr(), y2d.stride(0), rows, c,
-                               gamma.data_ptr(), beta.data_ptr(), eps, 1 if relu else 0, _stream()),
-          "prpe_layernorm")
+                               gamma.data_ptr(), beta.data_ptr(), eps, (1 if relu else 0) | (2 if planes else 0),
+                               _stream()), "prpe_layernorm")
     return y2d
 
 
@@ -146,13 +147,15 @@ def attention(qkv, out, B, L, H, D, scale):
     return out
 
 
-def attention_strided(qkv, strides, out, B, L, H, D, scale):
+def attention_strided(qkv, strides, out, B, L, H, D, scale, out_planes=False):
     """qkv: tensor holding q/k/v at element strides (frame, which, head, token), e.g. a
-    head-major [B, 3, H, L, D] buffer: (3*H*L*D, H*L*D, L*D, D)."""
+    head-major [B, 3, H, L, D] buffer: (3*H*L*D, H*L*D, L*D, D); the row-major [B*L, 3*H*D]
+    operand of prpe_attention is (L*3*H*D, H*D, D, 3*H*D). out_planes: write out in the planes
+    format (prpe.h) for a precision-0 GEMM consumer."""
     _gpu(qkv, out)
     sf, sw, sh, st = (int(v) for v in strides)
     check(lib().prpe_attention_strided(qkv.data_ptr(), sf, sw, sh, st, out.data_ptr(), B, L, H, D, scale,
-                                       _stream()), "prpe_attention_strided")
+                                       1 if out_planes else 0, _stream()), "prpe_attention_strided")
     return out
 
 

@@ -350,6 +350,47 @@ def test_conv_halo_kernel_bit_exact_vs_wave(B, Ci, H, W, Co, k, s, p, tile):
     assert torch.equal(a, b) and ya == yb
 
 
+GEMM_SHAPES = [
+    (2, 64, 13, 11, 256),       # M = 286: one full + one ragged 256-row tile, 2 K-steps
+    (3, 768, 8, 12, 768),       # ViT-like: K = 768, three column tiles
+    (1, 96, 40, 40, 512),       # M = 1600, odd K-step count
+]
+
+
+@pytest.mark.parametrize("tile", [40, 41, 42])
+@pytest.mark.parametrize("B,Ci,H,W,Co", GEMM_SHAPES)
+def test_conv_gemm_kernel_bit_exact_vs_wave(B, Ci, H, W, Co, tile):
+    """conv_gemm.hip (256 x 256 tile, A and B both LDS-DMA'd) == the wave kernel bit for bit:
+    fp32 and planes input, planes output, pre-activation residual, GELU, per-frame max|y|."""
+    x = rnd(B, Ci, H, W, seed=190)
+    w = rnd(Co, Ci, 1, 1, seed=191, scale=1.0 / math.sqrt(Ci))
+    sc = torch.rand(Co, generator=_g(192)) + 0.5
+    bi = rnd(Co, seed=193)
+    r = rnd(B, Co, H, W, seed=194)
+    kw = dict(act="gelu", scale=sc, bias=bi, precision=0, res=r, res_mode=RES_PRE)
+    got = run_conv(x, w, 1, 0, tile=tile, **kw)
+    assert torch.equal(got, run_conv(x, w, 1, 0, tile=28, **kw))
+    ref = ref_conv(x, w, 1, 0, act="gelu", scale=sc, bias=bi, res=r, res_mode=RES_PRE)
+    torch.testing.assert_close(got, ref, rtol=0, atol=_tol(x, w) * 2)
+    pk = pack.pack_conv("g", w, 1, 0, DEV, scale=sc, bias=bi, act="gelu")
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    xpl = torch.empty_like(xd)
+    ops.conv2d(xd, pack.pack_conv("i", torch.eye(Ci).view(Ci, Ci, 1, 1), 1, 0, DEV), xpl, precision=2,
+               y_planes=True)
+    outs = []
+    for t in (tile, 28):
+        y = torch.empty(B, H, W, Co, device=DEV)
+        ya = torch.zeros(B, device=DEV)
+        ops.conv2d(xpl, pk, y, precision=0, x_planes=True, tile=t, y_amax=ya)
+        ypl = torch.empty(B, H, W, Co, device=DEV)
+        ops.conv2d(xd, pk, ypl, precision=0, y_planes=True, tile=t)
+        outs.append((y, ya, ypl))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert torch.equal(outs[0][1].cpu(), frame_amax(outs[0][0]))
+
+
 @pytest.mark.parametrize("mode", [RES_PRE, RES_POST])
 @pytest.mark.parametrize("tile", [21, 23])
 def test_conv_wave_kernel_prologue_residual_prelu(mode, tile):
@@ -562,6 +603,30 @@ def test_upconv_planes_output_feeds_conv_bit_exact(hi_, wi, ho, wo, act):
     hi, lo = _decode_planes(upl.cpu())
     assert torch.equal(hi, u32.cpu().to(torch.bfloat16).float())
     assert torch.equal(y32.cpu(), ypl.cpu())
+
+
+def test_layernorm_and_attention_planes_output_bit_exact():
+    """LayerNorm / attention writing the planes format == their fp32 output split into
+    hi = RNE(v), lo = RNE(v - hi) (the consumer GEMM's own split), bit for bit."""
+    rows, c = 384, 768
+    x = rnd(rows, c, seed=201, scale=3.0).to(DEV)
+    g = (torch.rand(c, generator=_g(202)) + 0.5).to(DEV)
+    b = rnd(c, seed=203).to(DEV)
+    y32 = ops.layernorm(x, torch.empty(rows, c, device=DEV), g, b)
+    ypl = ops.layernorm(x, torch.empty(rows, c, device=DEV), g, b, planes=True)
+    B, L, H, D = 2, 192, 12, 64
+    qkv = rnd(B * L, 3 * H * D, seed=204, scale=2.0).to(DEV)
+    st = (L * 3 * H * D, H * D, D, 3 * H * D)
+    o32 = ops.attention_strided(qkv, st, torch.empty(B * L, H * D, device=DEV), B, L, H, D, D ** -0.5)
+    opl = ops.attention_strided(qkv, st, torch.empty(B * L, H * D, device=DEV), B, L, H, D, D ** -0.5,
+                                out_planes=True)
+    torch.cuda.synchronize()
+    for v32, vpl in ((y32, ypl), (o32, opl)):
+        n = v32.shape[0]
+        hi, lo = _decode_planes(vpl.cpu().view(n, 1, 1, -1))
+        v = v32.cpu().view(n, 1, 1, -1)
+        assert torch.equal(hi, v.to(torch.bfloat16).float())
+        assert torch.equal(lo, (v - hi).to(torch.bfloat16).float())
 
 
 def test_planes_format_rejected_outside_precision_0():
