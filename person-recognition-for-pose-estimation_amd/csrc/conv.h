@@ -127,9 +127,9 @@ bool conv_halo_eligible(const ConvK& kp, int prec, int km);
 bool conv_halo_auto(const ConvK& kp, int prec);   // the automatic choice's shape rule
 
 // 256-row GEMM kernel (conv_gemm.hip) for 1x1 / s1 convs over contiguous pixels, Co % 128 == 0,
-// precision 0 (fp32 or planes input); tiles 40..42.
+// precision 0 (fp32 or planes input) or 3; tiles 40..42.
 bool conv_gemm_eligible(const ConvK& kp, int prec);
-int conv_gemm_launch(const ConvK& kp, int tile, hipStream_t st);
+int conv_gemm_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 
 }  // namespace prpe_k

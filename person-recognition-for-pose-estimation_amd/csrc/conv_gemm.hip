@@ -28,8 +28,12 @@ namespace {
 
 constexpr int GBK = 32;
 
-template <int BN, int WM, int STAGES, bool APL>
+// F16: precision 3 (fp16 planes of the per-frame-scaled activations, the weights' fp16 planes
+// pre-scaled per output channel; the per-row inverse scale in the epilogue), as conv_wave.hip.
+template <int BN, int WM, int STAGES, bool APL, bool F16>
 __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
+  static_assert(!(APL && F16), "planes input is precision 0");
+  using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
   constexpr int NW = 8, BM = 256, NP = 2;
   constexpr int WN = NW / WM;                          // waves along N
   constexpr int WTN = BN / WN;                         // wave tile (BM / WM) x WTN
@@ -68,7 +72,7 @@ __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
       const int q = jb / (BN / 16), rb = jb % (BN / 16);
       const int nrow = rb * 16 + (lane >> 2);
       const int ch = (lane & 3) ^ swzF(nrow);
-      const uint16_t* plane = q == 0 ? p.whi : p.wlo;
+      const uint16_t* plane = F16 ? (q == 0 ? p.wh16 : p.wl16) : (q == 0 ? p.whi : p.wlo);
       src[i] = reinterpret_cast<const float*>(plane + (int64_t)(n0 + nrow) * p.k_pad + ch * 8);
       dst[i] = A_BYTES + (q * BN + rb * 16) * 64;
     }
@@ -85,6 +89,16 @@ __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // precision 3: scale of each A row this lane splits (its frame's max|x| bound)
+  float rsc[F16 ? TM : 1];
+  if constexpr (F16) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * (BM / WM) + i * 16 + fr;
+      rsc[i] = m < p.M ? ldexpf(1.f, 15 - f16_scale_exp(p.x_amax[m / p.HoWo])) : 1.f;
+    }
+  }
 
   const int nk = p.nk;
 #pragma unroll
@@ -106,13 +120,13 @@ __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
     const unsigned char* sa = lds + st * STAGE;
     const unsigned char* sb = sa + A_BYTES;
     // B fragments of the wave's 4 column blocks (both planes), held for the whole step
-    bf16x8 bfr[TN][NP];
+    frag_t bfr[TN][NP];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int nrow = wn * WTN + j * 16 + fr;
       const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
 #pragma unroll
-      for (int q = 0; q < NP; ++q) bfr[j][q] = *reinterpret_cast<const bf16x8*>(bp + q * BN * 64);
+      for (int q = 0; q < NP; ++q) bfr[j][q] = *reinterpret_cast<const frag_t*>(bp + q * BN * 64);
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -125,10 +139,19 @@ __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
       const unsigned char* ap = sa + row * 128;
       const f4 v0 = *reinterpret_cast<const f4*>(ap + (((2 * fg) ^ sw) << 4));
       const f4 v1 = *reinterpret_cast<const f4*>(ap + (((2 * fg + 1) ^ sw) << 4));
-      bf16x8 af[NP];
+      frag_t af[NP];
       if constexpr (APL) {
         af[0] = __builtin_bit_cast(bf16x8, v0);
         af[1] = __builtin_bit_cast(bf16x8, v1);
+      } else if constexpr (F16) {
+        unsigned long long p0[2], p1[2];
+        split_planes_f16(v0, rsc[i], p0);
+        split_planes_f16(v1, rsc[i], p1);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+          af[q] = __builtin_bit_cast(f16x8, u64x2{p0[q], p1[q]});
+        }
       } else {
         bf16x4 p0[NP], p1[NP];
         split_planes<NP>(v0, p0);
@@ -183,6 +206,7 @@ __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
     for (int e = 0; e < EB; ++e) {
       f4 v = *reinterpret_cast<const f4*>(ct + (rr0 + RPP * e) * CS + cc * 4);
       if (!ok[e]) continue;
+      if constexpr (F16) v = v * ldexpf(1.f, f16_scale_exp(p.x_amax[mm[e] / p.HoWo]) - 15);
       v = v * sc4 + bi4;
       if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];
 #pragma unroll
@@ -209,33 +233,38 @@ __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
 
 bool conv_gemm_eligible(const ConvK& kp, int prec) {
   // 1x1 / stride 1 / pad 0 over contiguous pixels (x, y, residual rows at one pixel stride),
-  // whole 32-channel K-steps, Co a multiple of 128, precision 0 (fp32 or planes input),
-  // vectorised epilogue, no prologue / dual input
+  // whole 32-channel K-steps, Co a multiple of 128, precision 0 (fp32 or planes input) or 3
+  // (fp32 input, fp16 planes + the input's per-frame max bound), vectorised epilogue, no
+  // prologue / dual input
   const bool xlin = kp.xsh == (int64_t)kp.Wi * kp.xsw && kp.xsn == (int64_t)kp.Hi * kp.xsh && kp.xsc == 1;
-  return prec == 0 && kp.KH == 1 && kp.KW == 1 && kp.stride == 1 && kp.pad == 0 && kp.Ci % GBK == 0 &&
+  const bool p0 = prec == 0 && kp.whi && kp.wlo;
+  const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.x_planes;
+  return (p0 || p3) && kp.KH == 1 && kp.KW == 1 && kp.stride == 1 && kp.pad == 0 && kp.Ci % GBK == 0 &&
          kp.K == kp.Ci && kp.k_pad == kp.K && kp.Co % 128 == 0 && kp.vec_out && kp.ylin && kp.rlin && xlin &&
-         !kp.in_scale && !kp.x2 && kp.xsw % 4 == 0 && kp.whi && kp.wlo;
+         !kp.in_scale && !kp.x2 && kp.xsw % 4 == 0;
 }
 
 template <int BN, int WM, int STAGES>
-int launch_gemm(const ConvK& kp0, hipStream_t st) {
+int launch_gemm(const ConvK& kp0, int prec, hipStream_t st) {
   if (kp0.Co % BN) return PRPE_EINVAL;
   ConvK kp = kp0;
   kp.tiles_n = kp.Co / BN;
   const int64_t nwg = (int64_t)((kp.M + 255) / 256) * kp.tiles_n;
   if (nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
-  if (kp.x_planes) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, true>), dim3(kp.nwg), dim3(512), 0, st, kp);
-  else hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false>), dim3(kp.nwg), dim3(512), 0, st, kp);
+  const dim3 g(kp.nwg), b(512);
+  if (prec == 3) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, true>), g, b, 0, st, kp);
+  else if (kp.x_planes) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, true, false>), g, b, 0, st, kp);
+  else hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, false>), g, b, 0, st, kp);
   return launch_status();
 }
 
 // tile 40 = auto (256 x 128, 3 stages), 41 = 256 x 256 (2 stages), 42 = 256 x 128 (2 stages)
-int conv_gemm_launch(const ConvK& kp, int tile, hipStream_t st) {
+int conv_gemm_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
   switch (tile) {
-    case 41: return launch_gemm<256, 2, 2>(kp, st);
-    case 42: return launch_gemm<128, 4, 2>(kp, st);
-    default: return launch_gemm<128, 4, 3>(kp, st);
+    case 41: return launch_gemm<256, 2, 2>(kp, prec, st);
+    case 42: return launch_gemm<128, 4, 2>(kp, prec, st);
+    default: return launch_gemm<128, 4, 3>(kp, prec, st);
   }
 }
 

@@ -694,9 +694,14 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const char* e = getenv("PRPE_CONV_GEMM");
     return e && e[0] == '0' ? 0 : 1;
   }();
-  if (tile >= 40 && tile < 50) return conv_gemm_eligible(kp, prec) ? conv_gemm_launch(kp, tile, st) : PRPE_EINVAL;
-  if (tile == 0 && gemm_on && kp.x_planes && kp.M >= (1 << 15) && conv_gemm_eligible(kp, prec))
-    return conv_gemm_launch(kp, 40, st);
+  if (tile >= 40 && tile < 50) return conv_gemm_eligible(kp, prec) ? conv_gemm_launch(kp, prec, tile, st) : PRPE_EINVAL;
+  static const int gemm_p3 = [] {
+    const char* e = getenv("PRPE_CONV_GEMM_P3");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  if (tile == 0 && gemm_on && (kp.x_planes || (prec == 3 && gemm_p3)) && kp.M >= (1 << 15) &&
+      conv_gemm_eligible(kp, prec))
+    return conv_gemm_launch(kp, prec, 40, st);
   if (tile >= 30 && tile < 40)
     return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;
   if (tile == 0 && halo_on && conv_halo_auto(kp, prec) && conv_halo_eligible(kp, prec, km))

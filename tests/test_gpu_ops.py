@@ -391,6 +391,21 @@ def test_conv_gemm_kernel_bit_exact_vs_wave(B, Ci, H, W, Co, tile):
     assert torch.equal(outs[0][1].cpu(), frame_amax(outs[0][0]))
 
 
+@pytest.mark.parametrize("B,Ci,H,W,Co", GEMM_SHAPES + [(3, 64, 5, 7, 256)])
+def test_conv_gemm_kernel_precision3_bit_exact_vs_wave(B, Ci, H, W, Co):
+    """precision 3 on the GEMM kernel (per-row frame scales; the last shape has 35-pixel frames,
+    so 256-row tiles straddle up to 8 frames) == the wave kernel's 128x128 tile, with the
+    per-frame max|y| slots and a residual."""
+    x = torch.relu(rnd(B, Ci, H, W, seed=195)) * torch.tensor([7.0, 0.01, 300.0][:B]).view(B, 1, 1, 1)
+    w = rnd(Co, Ci, 1, 1, seed=196, scale=1.0 / math.sqrt(Ci))
+    sc = torch.rand(Co, generator=_g(197)) + 0.5
+    bi = rnd(Co, seed=198)
+    r = rnd(B, Co, H, W, seed=199)
+    a, ya = _conv_p3(x, w, 1, 0, tile=40, scale=sc, bias=bi, act="relu", res=r, res_mode=RES_PRE)
+    b, yb = _conv_p3(x, w, 1, 0, tile=27, scale=sc, bias=bi, act="relu", res=r, res_mode=RES_PRE)
+    assert torch.equal(a, b) and ya == yb
+
+
 @pytest.mark.parametrize("mode", [RES_PRE, RES_POST])
 @pytest.mark.parametrize("tile", [21, 23])
 def test_conv_wave_kernel_prologue_residual_prelu(mode, tile):
