@@ -183,16 +183,7 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
     if constexpr (VW == 4) {
       if (p.y_planes) {
         // channel group c0 / 8 of the pixel: hi[8] then lo[8] (bf16 RNE two-plane split)
-        uint16_t* y16 = reinterpret_cast<uint16_t*>(y - c0) + (c0 >> 3) * 16 + (c0 & 7);
-        unsigned short hi[4], lo[4];
-#pragma unroll
-        for (int v = 0; v < 4; ++v) {
-          const __bf16 h = (__bf16)out[v];
-          hi[v] = __builtin_bit_cast(unsigned short, h);
-          lo[v] = __builtin_bit_cast(unsigned short, (__bf16)(out[v] - (float)h));
-        }
-        *reinterpret_cast<uint2*>(y16) = make_uint2(hi[0] | (unsigned)hi[1] << 16, hi[2] | (unsigned)hi[3] << 16);
-        *reinterpret_cast<uint2*>(y16 + 8) = make_uint2(lo[0] | (unsigned)lo[1] << 16, lo[2] | (unsigned)lo[3] << 16);
+        store_planes4(reinterpret_cast<uint16_t*>(y - c0), c0, f32x4{out[0], out[1], out[2], out[3]});
         continue;
       }
       if (p.y.sc == 1) {

@@ -757,11 +757,13 @@ def test_epilogue_activation_accuracy(act):
 
 
 @pytest.mark.parametrize("hi,wi,ho,wo,ac", [(20, 20, 160, 160, True), (20, 20, 256, 192, True),
-                                        (16, 12, 64, 48, False), (7, 9, 20, 13, False), (20, 20, 23, 21, True)])
+                                        (16, 12, 64, 48, False), (7, 9, 20, 13, False), (20, 20, 23, 21, True),
+                                        (20, 20, 112, 112, True), (9, 5, 40, 17, False), (13, 6, 37, 11, True),
+                                        (20, 7, 51, 9, False), (11, 4, 61, 8, True)])
 def test_upconv_fused_matches_separable(hi, wi, ho, wo, ac):
     """The one-pass rolling-row kernel and the two-pass separable form evaluate the same sum
     (FMA contraction may differ: fp32-rounding-level agreement), at the adapters' upsampling
-    ratios and at awkward ones (source intervals of 1-2 output rows)."""
+    ratios and at awkward ones (source intervals of 1-2 output rows, both align_corners modes)."""
     Co = 24
     z = rnd(2, hi, wi, 9 * Co, seed=103).to(DEV)
     sc = (torch.rand(Co, generator=_g(104)) + 0.5).to(DEV)
