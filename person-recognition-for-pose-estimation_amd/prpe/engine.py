@@ -379,6 +379,9 @@ class Engine:
                         act="silu", planes=True)
         t = self.conv(u, self.pk(a + ".7", a + ".7.weight", bn=a + ".8", bias_key=a + ".7.bias", act="silu"),
                       planes_out=True)
+        # .10 and .13 write fp32: the 64-column 1x1 below runs faster on the register-staged
+        # 256x64 tile than on the planes-input wave tile (1.12 vs 1.64 ms at bs=256), and the
+        # 27-column tap GEMM after .13 needs fp32 input
         t = self.conv(t, self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias",
                                  act="silu"))
         t = self.conv(t, self.pk(a + ".13", a + ".13.weight", bn=a + ".14", bias_key=a + ".13.bias", act="silu"))
@@ -453,9 +456,9 @@ class Engine:
         u = self.upconv(a + ".4", t, a + ".4.weight", (112, 112), True, bn=a + ".5", bias_key=a + ".4.bias",
                         act="prelu", prelu=a + ".6.weight", planes=True)
         t = self.conv(u, self.pk(a + ".7", a + ".7.weight", 1, 1, bn=a + ".8", bias_key=a + ".7.bias", act="prelu",
-                                 prelu=a + ".9.weight"))
+                                 prelu=a + ".9.weight"), planes_out=True)
         t = self.conv(t, self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias",
-                                 act="prelu", prelu=a + ".12.weight"))
+                                 act="prelu", prelu=a + ".12.weight"), planes_out=True)
         m = "ada_face.adaface_model"
         x = self.conv(t, self.pk(m + ".input_layer", m + ".input_layer.0.weight", 1, 1, bn=m + ".input_layer.1",
                                  act="prelu", prelu=m + ".input_layer.2.weight"))
