@@ -119,6 +119,14 @@ typedef struct prpe_conv_desc {
    * (channel-contiguous, C % 8 == 0, 32-B aligned). */
   int32_t x_planes;
   int32_t y_planes;
+  /* optional 1x1 GEMM in the epilogue (w2 != NULL): after scale/bias/act, z = y' W2^T with W2
+   * fp32 [y2.c][Co] (exact fp32 FMAs), written to y2 [N, Ho, Wo, n2] (channel-contiguous,
+   * n2 <= 32) instead of y (not written). The 3x3 conv -> Co <= 4 3x3 conv pairs of the
+   * adapters (the second conv as its 1x1 tap GEMM + shifted tap sum, prpe_upconv3x3 at unit
+   * scale): the intermediate tensor never reaches HBM. Haloed-tile 3x3 kernel only (3x3 / s1 /
+   * p1, Co <= 128, precision 0 planes input or 3). */
+  const float* w2;
+  prpe_view y2;
 } prpe_conv_desc;
 
 int prpe_conv2d(const prpe_conv_desc* d, void* stream);

@@ -31,6 +31,7 @@ struct ConvK {
   int nk1;                                      // K-steps of the first input
   const float* x2_amax;
   int x_planes, y_planes;                       // planes format input / output (conv_wave)
+  const float* w2; float* y2; int64_t y2sn, y2sh, y2sw; int n2;   // epilogue 1x1 GEMM (conv_halo)
 };
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));

@@ -32,7 +32,10 @@ namespace {
 
 constexpr int HBK = 32;
 
-template <int NW, int TR, int TC, int TN, bool F16, bool APL>
+// TAPS: the epilogue's activated tile (all Co <= BN columns of 16 rows at a time, in the wave's
+// LDS slice) is multiplied by w2 [n2][Co] (split-bf16 MFMAs, w2 split into LDS once per block)
+// and z is written to y2 instead of y (see prpe.h, w2).
+template <int NW, int TR, int TC, int TN, bool F16, bool APL, bool TAPS = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void conv_halo_kernel(ConvK p, int tiles_w, int tiles_h) {
   static_assert(TC % 16 == 0 && (TR * TC / 16) % NW == 0, "tile");
   static_assert(!(F16 && APL), "planes input is precision 0");
@@ -49,7 +52,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   constexpr int CS = BN + 4;
   constexpr int EPI = NW * 16 * CS * 4;
   constexpr int MAIN = 2 * HALO + 2 * B_STAGE;
-  constexpr int LDS_BYTES = MAIN > EPI ? MAIN : EPI;
+  constexpr int W2B = TAPS ? 2 * 32 * (BN + 8) * 2 : 0;  // w2 bf16 planes after the slabs
+  constexpr int LDS_BYTES = MAIN > EPI + W2B ? MAIN : EPI + W2B;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
   unsigned char* const halo0 = lds;
   unsigned char* const ring = lds + 2 * HALO;
@@ -204,6 +208,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
   }
   float ym = 0.f;
+  // TAPS: w2 split once into two bf16 planes [32][W2S] (rows >= n2 and columns >= Co zero)
+  constexpr int W2S = BN + 8;                          // padded row: 16-B shift per row
+  uint16_t* const w2s = reinterpret_cast<uint16_t*>(lds + EPI);
+  if constexpr (TAPS) {
+    for (int e = tid; e < 32 * BN / 4; e += NW * 64) {
+      const int r = e / (BN / 4), c = (e - r * (BN / 4)) * 4;
+      f4 v = {0.f, 0.f, 0.f, 0.f};
+      if (r < p.n2 && c < p.Co) v = *reinterpret_cast<const f4*>(p.w2 + r * p.Co + c);
+      bf16x4 pl[2];
+      split_planes<2>(v, pl);
+      *reinterpret_cast<bf16x4*>(w2s + r * W2S + c) = pl[0];
+      *reinterpret_cast<bf16x4*>(w2s + 32 * W2S + r * W2S + c) = pl[1];
+    }
+    __syncthreads();
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int rb = wave * TM + i;
@@ -237,6 +256,10 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
       if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
+      if constexpr (TAPS) {                            // keep the activated value for the tap GEMM
+        *reinterpret_cast<f4*>(ct + (rr0 + RPP * e) * CS + cc * 4) = v;
+        continue;
+      }
       if (p.y_planes) {
         bf16x4 pl[2];
         split_planes<2>(v, pl);
@@ -248,20 +271,58 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       }
       if (p.y_amax) ym = fmaxf(ym, amax4(v));
     }
+    if constexpr (TAPS) {
+      // z [16 pixels][32] = y' [16][BN] w2^T on the matrix cores, the two-plane (3-product)
+      // split as everywhere at precision 0: A = the activated slab rows, B = the w2 planes
+      __builtin_amdgcn_wave_barrier();
+      f32x4 zc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+      for (int kk = 0; kk < BN / 32; ++kk) {
+        const float* ap = ct + fr * CS + kk * 32 + fg * 8;
+        bf16x4 p0[2], p1[2];
+        split_planes<2>(*reinterpret_cast<const f4*>(ap), p0);
+        split_planes<2>(*reinterpret_cast<const f4*>(ap + 4), p1);
+        bf16x8 za[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          za[q] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
+#pragma unroll
+        for (int jn = 0; jn < 2; ++jn) {
+          const uint16_t* bp = w2s + (jn * 16 + fr) * W2S + kk * 32 + fg * 8;
+          const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(bp);
+          const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(bp + 32 * W2S);
+          zc[jn] = mfma16(za[1], b0, zc[jn]);
+          zc[jn] = mfma16(za[0], b1, zc[jn]);
+          zc[jn] = mfma16(za[0], b0, zc[jn]);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ow = owb + fg * 4 + r;
+        if (oh < p.Ho && ow < p.Wo) {
+          float* zo = p.y2 + (int64_t)n * p.y2sn + (int64_t)oh * p.y2sh + (int64_t)ow * p.y2sw;
+#pragma unroll
+          for (int jn = 0; jn < 2; ++jn)
+            if (jn * 16 + fr < p.n2) zo[jn * 16 + fr] = zc[jn][r];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
   }
   if (p.y_amax) amax_commit(p.y_amax + n, ym);
 }
 
-template <int NW, int TR, int TC, int TN, bool F16, bool APL>
+template <int NW, int TR, int TC, int TN, bool F16, bool APL, bool TAPS = false>
 int launch_halo(const ConvK& kp0, hipStream_t st) {
   ConvK kp = kp0;
+  if (kp.w2 && kp.Co > TN * 16) return PRPE_EINVAL;     // the tap GEMM needs every column in one tile
   const int tiles_w = (kp.Wo + TC - 1) / TC, tiles_h = (kp.Ho + TR - 1) / TR;
   kp.tiles_n = (kp.Co + TN * 16 - 1) / (TN * 16);
   const int64_t nwg = (int64_t)(kp.M / kp.HoWo) * tiles_h * tiles_w * kp.tiles_n;
   if (nwg <= 0 || nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
-  hipLaunchKernelGGL((conv_halo_kernel<NW, TR, TC, TN, F16, APL>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp, tiles_w,
-                     tiles_h);
+  hipLaunchKernelGGL((conv_halo_kernel<NW, TR, TC, TN, F16, APL, TAPS>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp,
+                     tiles_w, tiles_h);
   return launch_status();
 }
 
@@ -269,6 +330,13 @@ template <int NW, int TR, int TC, int TN>
 int launch_halo_kind(const ConvK& kp, int prec, hipStream_t st) {
   if (prec == 3) return launch_halo<NW, TR, TC, TN, true, false>(kp, st);
   return kp.x_planes ? launch_halo<NW, TR, TC, TN, false, true>(kp, st) : launch_halo<NW, TR, TC, TN, false, false>(kp, st);
+}
+
+// epilogue tap GEMM: the 8 x 16-pixel, 128-column tile
+int launch_halo_taps(const ConvK& kp, int prec, hipStream_t st) {
+  if (prec == 3) return launch_halo<4, 8, 16, 8, true, false, true>(kp, st);
+  return kp.x_planes ? launch_halo<4, 8, 16, 8, false, true, true>(kp, st)
+                     : launch_halo<4, 8, 16, 8, false, false, true>(kp, st);
 }
 
 }  // namespace
@@ -298,6 +366,7 @@ bool conv_halo_auto(const ConvK& kp, int prec) {
 // per workgroup, or 64 when Co <= 64 (tools/conv_bench.py, profiles/r02_conv_bench_halo.txt);
 // 31..35 force a configuration
 int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
+  if (kp.w2) return tile == 30 || tile == 31 ? launch_halo_taps(kp, prec, st) : PRPE_EINVAL;
   if (tile == 30) tile = kp.Co <= 64 ? 34 : 31;
   switch (tile) {
     case 31: return launch_halo_kind<4, 8, 16, 8>(kp, prec, st);     // 8 x 16 px, 4 waves, 128 ch

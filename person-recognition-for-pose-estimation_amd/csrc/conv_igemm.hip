@@ -634,6 +634,15 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
                       d->precision == 1))
     return PRPE_EINVAL;
   if (d->precision == 3) kp.scale = d->scale16;
+  // epilogue 1x1 GEMM (haloed-tile 3x3 kernel only)
+  if (d->w2 && d->tile != 0 && (d->tile < 30 || d->tile >= 40)) return PRPE_EINVAL;
+  if (d->w2) {
+    const prpe_view& v2 = d->y2;
+    if (!view_ok(&v2) || v2.n != y.n || v2.h != Ho || v2.w != Wo || v2.c > 32 || v2.sc != 1 || y.c > 128 ||
+        d->y_planes || d->res_mode != PRPE_RES_NONE || d->y_amax || (uintptr_t)d->w2 % 16 || y.c % 4)
+      return PRPE_EINVAL;
+    kp.w2 = d->w2; kp.y2 = v2.ptr; kp.y2sn = v2.sn; kp.y2sh = v2.sh; kp.y2sw = v2.sw; kp.n2 = v2.c;
+  }
   kp.ylin = y.sh == (int64_t)Wo * y.sw && y.sn == (int64_t)Ho * y.sh;
   kp.rlin = d->res_mode == PRPE_RES_NONE ||
             (d->res.sh == (int64_t)Wo * d->res.sw && d->res.sn == (int64_t)Ho * d->res.sh);
@@ -655,6 +664,8 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   // direct fp32 kernel for tiny Co (needs the 3 weight planes; exact fp32 products); 1x1 only:
   // for 3x3 Co=3 the MFMA path measured faster (7.5 ms vs 11.8 ms at bs=256)
   const int khw = d->kh * d->kw;
+  // epilogue 1x1 GEMM: the haloed-tile kernel's 128-column tile is the only implementation
+  if (kp.w2) return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile ? tile : 31, st) : PRPE_EINVAL;
   if (tile == 0 && y.c <= 4 && km == 1 && !d->in_scale && d->w_lo && d->w_lo2 && x.c <= 256 && khw == 1) {
     int lg = 0;
     while ((1 << lg) * 4 < x.c) ++lg;

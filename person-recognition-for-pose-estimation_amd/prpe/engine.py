@@ -45,6 +45,10 @@ PLANES_ON = os.environ.get("PRPE_PLANES", "1") != "0"
 # at unit scale: one read of the input by a 1x1 GEMM to the 9*Co tap maps, then a shifted tap
 # sum (prpe_upconv3x3 with an identity resample). PRPE_SMALLCO_TAPS=0 keeps the direct conv.
 SMALLCO_TAPS = os.environ.get("PRPE_SMALLCO_TAPS", "1") != "0"
+# ... and where the producer of that conv's input is a haloed-tile 3x3 conv (ViTPose adapter.7 ->
+# .10), the tap GEMM runs in the producer's epilogue (prpe_conv_desc.w2): the 128-channel map
+# never reaches HBM. PRPE_TAPS_FUSE=0 runs the two convs separately.
+TAPS_FUSE = os.environ.get("PRPE_TAPS_FUSE", "1") != "0"
 
 
 class _Prec:
@@ -158,9 +162,10 @@ class Engine:
         return p
 
     def conv(self, x, p: ConvPack, out=None, res=None, res_mode=0, act=None, x2=None, x2_amax=None,
-             planes_out=False):
+             planes_out=False, w2=None, y2=None):
         """``x2``: second 1x1 input on the output grid (dual-input GEMM, see prpe.h).
-        ``planes_out``: the only consumer is a precision-0 wave-row conv: write the planes format."""
+        ``planes_out``: the only consumer is a precision-0 wave-row conv: write the planes format.
+        ``w2``/``y2``: epilogue 1x1 GEMM into y2 (prpe.h); ``out`` is then not written."""
         B, H, W, _ = x.shape
         Ho = (H + 2 * p.pad - p.kh) // p.stride + 1
         Wo = (W + 2 * p.pad - p.kw) // p.stride + 1
@@ -170,13 +175,13 @@ class Engine:
         if prec == 3 and (not self._f16_ok(x, p, out) or (x2 is not None and x2_amax is None)):
             prec = 2
         xa = getattr(x, "_prpe_amax", None) if prec == 3 else None
-        ya = self.amax_slot(B) if self.precision == 3 else None
+        ya = self.amax_slot(B) if self.precision == 3 and w2 is None else None
         x_planes = getattr(x, "_prpe_planes", False)
         if x_planes and prec != 0:
             raise RuntimeError(f"{p.name}: planes-format input needs precision 0, got {prec}")
         y_planes = PLANES_ON and planes_out and prec == 0 and p.co % 8 == 0 and out.is_contiguous()
         kw = dict(res=res, res_mode=res_mode, act=act, precision=prec, tile=p.tile, x_amax=xa, y_amax=ya, x2=x2,
-                  x2_amax=x2_amax if prec == 3 else None, x_planes=x_planes, y_planes=y_planes)
+                  x2_amax=x2_amax if prec == 3 else None, x_planes=x_planes, y_planes=y_planes, w2=w2, y2=y2)
         if p.name in self.watch:          # HIP events around one kernel (bench roofline)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -191,10 +196,11 @@ class Engine:
         return out
 
     def upconv(self, name, x, wkey, size, align_corners, bn=None, bias_key=None, act="none", prelu=None, out=None,
-               planes=False):
+               planes=False, z=None):
         """conv3x3(pad 1)(bilinear_upsample(x, size)) [+BN] [+act] via the tap rewrite.
         ``planes``: the only consumer is a precision-0 conv, so write the planes format (the
-        consumer's two-plane split done once here; include/prpe.h)."""
+        consumer's two-plane split done once here; include/prpe.h).
+        ``z``: the tap GEMM's output, already computed (``x`` is then unused)."""
         taps = self._packs.get(name + ":taps")
         if taps is None:
             taps = pack_upconv_taps(name + ":taps", self.sd[wkey], self.device)
@@ -209,8 +215,9 @@ class Engine:
                 s, b = torch.ones(co), (cb if cb is not None else torch.zeros(co))
             self._aux[key] = s.float().to(self.device)
             self._aux[key + "b"] = b.float().contiguous().to(self.device)
-        z = self.conv(x, taps)
-        B = x.shape[0]
+        if z is None:
+            z = self.conv(x, taps)
+        B = z.shape[0]
         if out is None:
             out = self.empty(B, size[0], size[1], co)
         slope = self.dev(prelu) if prelu else None
@@ -500,7 +507,19 @@ class Engine:
         t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="gelu"))
         u = self.upconv(a + ".4", t, a + ".4.weight", arch.VIT_IMG, True, bn=a + ".5", bias_key=a + ".4.bias",
                         act="gelu", planes=True)
-        t = self.conv(u, self.pk(a + ".7", a + ".7.weight", 1, 1, bn=a + ".8", bias_key=a + ".7.bias", act="gelu"))
+        p7 = self.pk(a + ".7", a + ".7.weight", 1, 1, bn=a + ".8", bias_key=a + ".7.bias", act="gelu")
+        if SMALLCO_TAPS and TAPS_FUSE and getattr(u, "_prpe_planes", False):
+            # .7's epilogue computes .10's tap GEMM (w2 = .10's weight as [(tap, co), ci], the
+            # pack_upconv_taps order); its 128-channel output exists only in LDS
+            w2 = self.dev(a + ".10:w2", lambda: self.sd[a + ".10.weight"].float().permute(2, 3, 0, 1)
+                          .reshape(-1, p7.co).contiguous())
+            B, H, W, _ = u.shape
+            z = self.empty(B, H, W, w2.shape[0])
+            sink = self.dev("sink:" + str(p7.co), lambda: torch.zeros(p7.co)).expand(B, H, W, p7.co)
+            self.conv(u, p7, out=sink, w2=w2, y2=z)
+            return self.upconv(a + ".10", None, a + ".10.weight", (H, W), True, bn=a + ".11",
+                               bias_key=a + ".10.bias", act="gelu", z=z)
+        t = self.conv(u, p7)
         return self.conv3x3_smallco(t, a + ".10", a + ".10.weight", bn=a + ".11", bias_key=a + ".10.bias",
                                     act="gelu")
 

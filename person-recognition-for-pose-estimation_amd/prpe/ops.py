@@ -47,7 +47,7 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
 
 
 def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, tile=0, x_amax=None,
-           y_amax=None, x2=None, x2_amax=None, x_planes=False, y_planes=False):
+           y_amax=None, x2=None, x2_amax=None, x_planes=False, y_planes=False, w2=None, y2=None):
     """y = EPI(conv(PRO(x))) with a ``ConvPack`` (see prpe.pack).
 
     precision 3 (split fp16) needs ``x_amax``: a [N] device tensor, x_amax[n] bounding max|x[n]|
@@ -65,6 +65,12 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
         d.x_amax = _ptr(x_amax)
     d.y_amax = _ptr(y_amax)
     d.x_planes, d.y_planes = int(x_planes), int(y_planes)   # planes format, see prpe.h
+    if w2 is not None:                 # epilogue 1x1 GEMM (w2 fp32 [n2][Co]) into y2, see prpe.h
+        _gpu(w2, y2)
+        if w2.dtype != torch.float32 or not w2.is_contiguous() or w2.shape != (y2.shape[3], y.shape[3]):
+            raise ValueError(f"prpe_conv2d[{pack.name}]: w2 must be contiguous float32 [n2, Co]")
+        d.w2 = w2.data_ptr()
+        d.y2 = view(y2)
     if x2 is not None:                 # second 1x1 input, see prpe.h (dual input)
         d.x2 = view(x2)
         d.x2_amax = _ptr(x2_amax)

@@ -350,6 +350,56 @@ def test_conv_halo_kernel_bit_exact_vs_wave(B, Ci, H, W, Co, k, s, p, tile):
     assert torch.equal(a, b) and ya == yb
 
 
+TAPS_SHAPES = [
+    (2, 64, 17, 19, 128, 27),   # ragged tiles, the adapter's n2 = 9 taps x 3 channels
+    (1, 256, 24, 20, 96, 12),   # Co < 128 (zero-padded w2 columns), 8 chunks
+    (2, 32, 9, 33, 64, 32),     # one chunk, the widest n2
+]
+
+
+@pytest.mark.parametrize("mode", ["fp32", "planes", "p3"])
+@pytest.mark.parametrize("B,Ci,H,W,Co,n2", TAPS_SHAPES)
+def test_conv_halo_taps_epilogue(B, Ci, H, W, Co, n2, mode):
+    """prpe_conv_desc.w2: the haloed-tile kernel's epilogue multiplies its activated tile by
+    w2^T on the matrix cores (two bf16 planes per operand, three products: the precision-0
+    split) and writes z = y' w2^T to y2 (y untouched). y' is the same conv's unfused output
+    (same kernel, bit-identical accumulation), so z is checked against y' w2^T in fp64 within
+    the split's bound: each operand carries <= 2^-16 relative residual after two bf16 planes,
+    plus fp32 accumulation (2^-24 per term): 2^-14 * sum_k |y'_k w2_ck| covers both."""
+    x = rnd(B, Ci, H, W, seed=190)
+    if mode == "p3":
+        x = torch.relu(x) * 5.0
+    w = rnd(Co, Ci, 3, 3, seed=191, scale=1.0 / math.sqrt(Ci * 9))
+    sc = torch.rand(Co, generator=_g(192)) + 0.5
+    bi = rnd(Co, seed=193)
+    w2 = rnd(n2, Co, seed=194).to(DEV)
+    pk = pack.pack_conv("t", w, 1, 1, DEV, scale=sc, bias=bi, act="gelu", k_order=1)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    kw = dict(precision=0)
+    if mode == "planes":
+        xpl = torch.empty_like(xd)
+        ops.conv2d(xd, pack.pack_conv("i", torch.eye(Ci).view(Ci, Ci, 1, 1), 1, 0, DEV), xpl, precision=2,
+                   y_planes=True)
+        xd, kw = xpl, dict(precision=0, x_planes=True)
+    elif mode == "p3":
+        kw = dict(precision=3, x_amax=frame_amax(x).to(DEV))
+    y = torch.empty(B, H, W, Co, device=DEV)
+    ops.conv2d(xd, pk, y, tile=31, **kw)
+    sink = torch.full((B, H, W, Co), float("nan"), device=DEV)
+    z = torch.full((B, H, W, n2), float("nan"), device=DEV)
+    ops.conv2d(xd, pk, sink, w2=w2, y2=z, **kw)
+    torch.cuda.synchronize()
+    assert torch.isnan(sink).all()
+    yd, wd = y.double().cpu(), w2.double().cpu()
+    ref = yd @ wd.T
+    bound = (yd.abs() @ wd.abs().T) * 2.0 ** -14
+    err = (z.double().cpu() - ref).abs()
+    assert torch.isfinite(z).all() and bool((err <= bound).all()), float((err / bound.clamp_min(1e-30)).max())
+    # only the haloed-tile kernel implements it
+    with pytest.raises(PrpeError):
+        ops.conv2d(xd, pk, sink, w2=w2, y2=z, tile=28, **kw)
+
+
 GEMM_SHAPES = [
     (2, 64, 13, 11, 256),       # M = 286: one full + one ragged 256-row tile, 2 K-steps
     (3, 768, 8, 12, 768),       # ViT-like: K = 768, three column tiles
