@@ -89,6 +89,8 @@ __device__ __forceinline__ void split_bf16(float x, __bf16& hi, __bf16& lo) {
 // row16: the pixel's first bf16 slot. The remainder is an explicit v_sub_f32: with FP
 // contraction the compiler would fuse a producing multiply into it (fma(a, b, -hi)) and the
 // planes would no longer be the split of the stored fp32 value.
+// NT: non-temporal stores (streaming; the output is not re-read by this kernel)
+template <bool NT = false>
 __device__ __forceinline__ void store_planes4(uint16_t* row16, int c, f32x4 v) {
   uint16_t* y16 = row16 + (c >> 3) * 16 + (c & 7);
   unsigned short hi[4], lo[4];
@@ -101,8 +103,17 @@ __device__ __forceinline__ void store_planes4(uint16_t* row16, int c, f32x4 v) {
     hi[e] = __builtin_bit_cast(unsigned short, h);
     lo[e] = __builtin_bit_cast(unsigned short, (__bf16)d);
   }
-  *reinterpret_cast<uint2*>(y16) = make_uint2(hi[0] | (unsigned)hi[1] << 16, hi[2] | (unsigned)hi[3] << 16);
-  *reinterpret_cast<uint2*>(y16 + 8) = make_uint2(lo[0] | (unsigned)lo[1] << 16, lo[2] | (unsigned)lo[3] << 16);
+  const unsigned long long h64 = (unsigned long long)(hi[0] | (unsigned)hi[1] << 16) |
+                                 (unsigned long long)(hi[2] | (unsigned)hi[3] << 16) << 32;
+  const unsigned long long l64 = (unsigned long long)(lo[0] | (unsigned)lo[1] << 16) |
+                                 (unsigned long long)(lo[2] | (unsigned)lo[3] << 16) << 32;
+  if constexpr (NT) {
+    __builtin_nontemporal_store(h64, reinterpret_cast<unsigned long long*>(y16));
+    __builtin_nontemporal_store(l64, reinterpret_cast<unsigned long long*>(y16 + 8));
+  } else {
+    *reinterpret_cast<unsigned long long*>(y16) = h64;
+    *reinterpret_cast<unsigned long long*>(y16 + 8) = l64;
+  }
 }
 
 __device__ __forceinline__ float warp_sum(float v) {

@@ -52,6 +52,7 @@ struct UpK {
   int per_row;    // Wo * (Co / VW)
   int chunks;     // ceil(per_row / 256)
   int y_planes;   // write y in the planes format (include/prpe.h, prpe_conv_desc)
+  int xcd;        // fused kernel: XCD-contiguous block order
 };
 
 // Fused one-pass form (no workspace). One thread = VW channels of one output column, for a
@@ -97,10 +98,15 @@ __device__ __forceinline__ void up_hrow(const float* __restrict__ zrow, const Up
 
 // ACT >= 0: the epilogue activation as a compile-time constant (one activation's code and
 // registers per instantiation); -1 reads p.act
-template <int VW, int ACT>
+// ABL (diagnostic builds, PRPE_UPCONV_ABL): 1 = no z loads (H rows from registers), 2 = no y
+// stores (kept live through a never-true condition), 3 = both
+template <int VW, int ACT, int ABL = 0>
 __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rblocks) {
-  const int chunk = blockIdx.x % p.chunks;
-  const int rb_n = blockIdx.x / p.chunks;
+  // XCD-aware order (p.xcd): consecutive chunks share their z source columns, so each XCD
+  // takes a contiguous range of the logical blocks instead of every 8th one
+  const int bid = p.xcd ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const int chunk = bid % p.chunks;
+  const int rb_n = bid / p.chunks;
   const int n = rb_n / rblocks, oy0 = (rb_n - n * rblocks) * R;
   const int j = chunk * 256 + threadIdx.x;
   const int Ho = p.y.h, Hi = p.z.h, Wo = p.y.w, Wi = p.z.w;
@@ -164,13 +170,21 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
       const int y1 = y0 < Hi - 1 ? y0 + 1 : y0;
       if (y0 != cur[dy]) {
         const float* zt = zn + dy * tap_row;
-        if (y0 == cur[dy] + 1) {
+        if constexpr ((ABL & 1) != 0) {
 #pragma unroll
-          for (int v = 0; v < VW; ++v) hA[dy][v] = hB[dy][v];
+          for (int v = 0; v < VW; ++v) {
+            hA[dy][v] = hB[dy][v];
+            hB[dy][v] = ux[v % 3].l1 * (float)(y1 + v);
+          }
         } else {
-          up_hrow<VW>(zt + (int64_t)y0 * p.z.sh, ux, xvalid, hA[dy], zsc);
+          if (y0 == cur[dy] + 1) {
+#pragma unroll
+            for (int v = 0; v < VW; ++v) hA[dy][v] = hB[dy][v];
+          } else {
+            up_hrow<VW>(zt + (int64_t)y0 * p.z.sh, ux, xvalid, hA[dy], zsc);
+          }
+          up_hrow<VW>(zt + (int64_t)y1 * p.z.sh, ux, xvalid, hB[dy], zsc);
         }
-        up_hrow<VW>(zt + (int64_t)y1 * p.z.sh, ux, xvalid, hB[dy], zsc);
         cur[dy] = y0;
       }
 #pragma unroll
@@ -180,14 +194,20 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
 #pragma unroll
     for (int v = 0; v < VW; ++v) out[v] = apply_act(acc[v] * sc[v] + bi[v], ACT >= 0 ? ACT : p.act, sl[v]);
     float* y = yn + (int64_t)oy * p.y.sh + yo;
+    if constexpr ((ABL & 2) != 0) {
+      if (out[0] + out[VW - 1] == 12345.678f) y[0] = out[0];
+      continue;
+    }
+    // non-temporal stores: the output is not re-read here, and z's lines stay in L2
+    // (-6 % on the adapters' shapes, tools/upconv_bench.py)
     if constexpr (VW == 4) {
       if (p.y_planes) {
         // channel group c0 / 8 of the pixel: hi[8] then lo[8] (bf16 RNE two-plane split)
-        store_planes4(reinterpret_cast<uint16_t*>(y - c0), c0, f32x4{out[0], out[1], out[2], out[3]});
+        store_planes4<true>(reinterpret_cast<uint16_t*>(y - c0), c0, f32x4{out[0], out[1], out[2], out[3]});
         continue;
       }
       if (p.y.sc == 1) {
-        *reinterpret_cast<float4*>(y) = make_float4(out[0], out[1], out[2], out[3]);
+        __builtin_nontemporal_store(f32x4{out[0], out[1], out[2], out[3]}, reinterpret_cast<f32x4*>(y));
         continue;
       }
     }
@@ -701,7 +721,29 @@ extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t al
   if (span(z) >= (1LL << 31) || span(y) >= (1LL << 31) || z->sw < 0 || z->sc < 0 || z->sh < 0 || y->sw < 0 ||
       y->sc < 0)
     return PRPE_EINVAL;
+  static const int xcd_env = [] {
+    const char* e = getenv("PRPE_UPCONV_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  p.xcd = xcd_env;
   const dim3 g((unsigned)nb);
+  static const int abl = [] {
+    const char* e = getenv("PRPE_UPCONV_ABL");
+    return e ? atoi(e) : 0;
+  }();
+#define PRPE_UP_ABL(A)                                                                                     \
+  if (abl == 1) hipLaunchKernelGGL((upconv_fused_kernel<4, A, 1>), g, dim3(256), 0, st, p, R, rblocks);     \
+  else if (abl == 2) hipLaunchKernelGGL((upconv_fused_kernel<4, A, 2>), g, dim3(256), 0, st, p, R, rblocks); \
+  else hipLaunchKernelGGL((upconv_fused_kernel<4, A, 3>), g, dim3(256), 0, st, p, R, rblocks);
+  if (abl && v4 && act == PRPE_ACT_SILU) {
+    PRPE_UP_ABL(PRPE_ACT_SILU)
+    return launch_status();
+  }
+  if (abl && v4 && act == PRPE_ACT_GELU) {
+    PRPE_UP_ABL(PRPE_ACT_GELU)
+    return launch_status();
+  }
+#undef PRPE_UP_ABL
   if (!v4) hipLaunchKernelGGL((upconv_fused_kernel<1, -1>), g, dim3(256), 0, st, p, R, rblocks);
   else if (act == PRPE_ACT_NONE) hipLaunchKernelGGL((upconv_fused_kernel<4, PRPE_ACT_NONE>), g, dim3(256), 0, st, p, R, rblocks);
   else if (act == PRPE_ACT_SILU) hipLaunchKernelGGL((upconv_fused_kernel<4, PRPE_ACT_SILU>), g, dim3(256), 0, st, p, R, rblocks);

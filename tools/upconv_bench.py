@@ -41,6 +41,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--fused-only", action="store_true")
     a = ap.parse_args()
     dev = "cuda"
     B = a.batch
@@ -55,9 +56,13 @@ def main():
         hbytes = 3 * B * Hi * Wo * Co * 4
         ms_copy = timeit(lambda: y2.copy_(y), a.iters)
         print(f"{name:34s} copy(y)            {ms_copy:8.3f} ms  {2 * ybytes / ms_copy / 1e6:8.1f} GB/s", flush=True)
-        for sep in (True, False):
-            for variant in ("plain", "epi"):
-                kw = dict(scale=sc, bias=bi, slope=sl if act == "prelu" else None, act=act) if variant == "epi" else {}
+        for sep in ((False,) if a.fused_only else (True, False)):
+            for variant in ("plain", "epi") + (() if sep else ("planes",)):
+                kw = dict(scale=sc, bias=bi, slope=sl if act == "prelu" else None, act=act) if variant != "plain" else {}
+                if variant == "planes":
+                    if Co % 8:
+                        continue
+                    kw["y_planes"] = True
                 ms = timeit(lambda: ops.upconv3x3(z, y, ac, separable=sep, **kw), a.iters)
                 alg = z.numel() * 4 + ybytes + (2 * hbytes if sep else 0)
                 print(f"{name:34s} {'sep' if sep else 'fused':6s} {variant:5s}       {ms:8.3f} ms  "
