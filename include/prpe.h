@@ -120,13 +120,22 @@ typedef struct prpe_conv_desc {
   int32_t x_planes;
   int32_t y_planes;
   /* optional 1x1 GEMM in the epilogue (w2 != NULL): after scale/bias/act, z = y' W2^T with W2
-   * fp32 [y2.c][Co] (exact fp32 FMAs), written to y2 [N, Ho, Wo, n2] (channel-contiguous,
-   * n2 <= 32) instead of y (not written). The 3x3 conv -> Co <= 4 3x3 conv pairs of the
-   * adapters (the second conv as its 1x1 tap GEMM + shifted tap sum, prpe_upconv3x3 at unit
-   * scale): the intermediate tensor never reaches HBM. Haloed-tile 3x3 kernel only (3x3 / s1 /
-   * p1, Co <= 128, precision 0 planes input or 3). */
+   * fp32 [y2.c][Co], written to y2 [N, Ho, Wo, y2.c] (channel-contiguous, y2.c <= 32) instead
+   * of y (not written). Split-bf16 matrix-core products (two planes per operand, three
+   * products: the precision-0 split) on the tile held in LDS. The 3x3 conv -> Co <= 4 3x3 conv
+   * pairs of the adapters (the second conv as its 1x1 tap GEMM + shifted tap sum,
+   * prpe_upconv3x3 at unit scale): the intermediate tensor never reaches HBM. Haloed-tile 3x3
+   * kernel only (3x3 / s1 / p1, Co <= 128, precision 0 or 3, no residual / planes / max|y|). */
   const float* w2;
   prpe_view y2;
+  /* optional second stage (w3 != NULL, with w2): z1 = act2(scale2 * (y' W2^T) + bias2) with
+   * W2 fp32 [n2][Co], n2 <= 64 (scale2 / bias2 [n2] or NULL for 1 / 0), then z = z1 W3^T with
+   * W3 fp32 [y2.c][n2] into y2 (a conv -> 1x1 conv -> tap GEMM chain, YOLO adapter .10/.13/.16) */
+  const float* w3;
+  const float* scale2;
+  const float* bias2;
+  int32_t act2;
+  int32_t n2;
 } prpe_conv_desc;
 
 int prpe_conv2d(const prpe_conv_desc* d, void* stream);

@@ -32,6 +32,7 @@ struct ConvK {
   const float* x2_amax;
   int x_planes, y_planes;                       // planes format input / output (conv_wave)
   const float* w2; float* y2; int64_t y2sn, y2sh, y2sw; int n2;   // epilogue 1x1 GEMM (conv_halo)
+  const float* w3; const float* s2; const float* b2; int act2; int nmid;     // its second stage
 };
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));

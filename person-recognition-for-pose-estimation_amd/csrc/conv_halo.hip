@@ -32,10 +32,56 @@ namespace {
 
 constexpr int HBK = 32;
 
-// TAPS: the epilogue's activated tile (all Co <= BN columns of 16 rows at a time, in the wave's
-// LDS slice) is multiplied by w2 [n2][Co] (split-bf16 MFMAs, w2 split into LDS once per block)
-// and z is written to y2 instead of y (see prpe.h, w2).
-template <int NW, int TR, int TC, int TN, bool F16, bool APL, bool TAPS = false>
+// 16-row slab GEMM of the epilogue: zc[jn] (16 x 16, jn < NTN) = slab[16][K] x W^T, W held as
+// two bf16 planes (row stride ws, plane stride ps) in LDS; A split into two planes here; three
+// products (precision 0). Lane layout as the main loop's 16x16x32 MFMA.
+template <int NTN, int K>
+__device__ __forceinline__ void slab_gemm(const float* ct, int cs, const uint16_t* w, int ws, int ps, int fr, int fg,
+                                          f32x4 (&zc)[NTN]) {
+#pragma unroll
+  for (int jn = 0; jn < NTN; ++jn) zc[jn] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kk = 0; kk < K / 32; ++kk) {
+    const float* ap = ct + fr * cs + kk * 32 + fg * 8;
+    bf16x4 p0[2], p1[2];
+    split_planes<2>(*reinterpret_cast<const f4*>(ap), p0);
+    split_planes<2>(*reinterpret_cast<const f4*>(ap + 4), p1);
+    bf16x8 za[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+      za[q] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
+#pragma unroll
+    for (int jn = 0; jn < NTN; ++jn) {
+      const uint16_t* bp = w + (jn * 16 + fr) * ws + kk * 32 + fg * 8;
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(bp);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(bp + ps);
+      zc[jn] = mfma16(za[1], b0, zc[jn]);
+      zc[jn] = mfma16(za[0], b1, zc[jn]);
+      zc[jn] = mfma16(za[0], b0, zc[jn]);
+    }
+  }
+}
+
+// fp32 [rows][cols] (row-major, ld) -> two bf16 planes [R][ws] in LDS (zero outside rows x cols)
+template <int R, int C>
+__device__ __forceinline__ void stage_planes(const float* w, int rows, int cols, int ld, uint16_t* dst, int ws,
+                                             int tid, int nthr) {
+  for (int e = tid; e < R * C / 4; e += nthr) {
+    const int r = e / (C / 4), c = (e - r * (C / 4)) * 4;
+    f4 v = {0.f, 0.f, 0.f, 0.f};
+    if (r < rows && c < cols) v = *reinterpret_cast<const f4*>(w + r * ld + c);
+    bf16x4 pl[2];
+    split_planes<2>(v, pl);
+    *reinterpret_cast<bf16x4*>(dst + r * ws + c) = pl[0];
+    *reinterpret_cast<bf16x4*>(dst + R * ws + r * ws + c) = pl[1];
+  }
+}
+
+// TAPS 1: the epilogue's activated tile (all Co <= BN columns of 16 rows at a time, in the
+// wave's LDS slice) is multiplied by w2 [n2][Co] (split-bf16 MFMAs, w2 split into LDS once per
+// block) and z is written to y2 instead of y. TAPS 2: z1 = act2(s2 (y' w2^T) + b2) with w2
+// [nmid <= 64][Co] first, back into the slice, then z = z1 w3^T (see prpe.h, w2 / w3).
+template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void conv_halo_kernel(ConvK p, int tiles_w, int tiles_h) {
   static_assert(TC % 16 == 0 && (TR * TC / 16) % NW == 0, "tile");
   static_assert(!(F16 && APL), "planes input is precision 0");
@@ -52,7 +98,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   constexpr int CS = BN + 4;
   constexpr int EPI = NW * 16 * CS * 4;
   constexpr int MAIN = 2 * HALO + 2 * B_STAGE;
-  constexpr int W2B = TAPS ? 2 * 32 * (BN + 8) * 2 : 0;  // w2 bf16 planes after the slabs
+  // w2 (and w3) bf16 planes after the slabs
+  constexpr int W2R = TAPS == 2 ? 64 : 32;
+  constexpr int W2B = TAPS ? 2 * W2R * (BN + 8) * 2 + (TAPS == 2 ? 2 * 32 * 72 * 2 : 0) : 0;
   constexpr int LDS_BYTES = MAIN > EPI + W2B ? MAIN : EPI + W2B;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
   unsigned char* const halo0 = lds;
@@ -208,20 +256,26 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
   }
   float ym = 0.f;
-  // TAPS: w2 split once into two bf16 planes [32][W2S] (rows >= n2 and columns >= Co zero)
-  constexpr int W2S = BN + 8;                          // padded row: 16-B shift per row
+  // TAPS: w2 (w3) split once into two bf16 planes (rows / columns beyond the real ones zero)
+  constexpr int W2S = BN + 8, W3S = 72;                // padded rows: 16-B shift per row
   uint16_t* const w2s = reinterpret_cast<uint16_t*>(lds + EPI);
-  if constexpr (TAPS) {
-    for (int e = tid; e < 32 * BN / 4; e += NW * 64) {
-      const int r = e / (BN / 4), c = (e - r * (BN / 4)) * 4;
-      f4 v = {0.f, 0.f, 0.f, 0.f};
-      if (r < p.n2 && c < p.Co) v = *reinterpret_cast<const f4*>(p.w2 + r * p.Co + c);
-      bf16x4 pl[2];
-      split_planes<2>(v, pl);
-      *reinterpret_cast<bf16x4*>(w2s + r * W2S + c) = pl[0];
-      *reinterpret_cast<bf16x4*>(w2s + 32 * W2S + r * W2S + c) = pl[1];
-    }
+  uint16_t* const w3s = w2s + 2 * W2R * W2S;
+  if constexpr (TAPS != 0) {
+    stage_planes<W2R, BN>(p.w2, TAPS == 2 ? p.nmid : p.n2, p.Co, p.Co, w2s, W2S, tid, NW * 64);
+    if constexpr (TAPS == 2) stage_planes<32, 64>(p.w3, p.n2, p.nmid, p.nmid, w3s, W3S, tid, NW * 64);
     __syncthreads();
+  }
+  // TAPS 2: this lane's middle columns jn * 16 + fr
+  f32x4 s2 = {0.f, 0.f, 0.f, 0.f}, b2 = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (TAPS == 2) {
+#pragma unroll
+    for (int jn = 0; jn < 4; ++jn) {
+      const int c = jn * 16 + fr;
+      if (c < p.nmid) {
+        s2[jn] = p.s2 ? p.s2[c] : 1.f;
+        b2[jn] = p.b2 ? p.b2[c] : 0.f;
+      }
+    }
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -256,7 +310,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
       for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
       if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
-      if constexpr (TAPS) {                            // keep the activated value for the tap GEMM
+      if constexpr (TAPS != 0) {                       // keep the activated value for the tap GEMM
         *reinterpret_cast<f4*>(ct + (rr0 + RPP * e) * CS + cc * 4) = v;
         continue;
       }
@@ -271,30 +325,24 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       }
       if (p.y_amax) ym = fmaxf(ym, amax4(v));
     }
-    if constexpr (TAPS) {
+    if constexpr (TAPS != 0) {
       // z [16 pixels][32] = y' [16][BN] w2^T on the matrix cores, the two-plane (3-product)
       // split as everywhere at precision 0: A = the activated slab rows, B = the w2 planes
       __builtin_amdgcn_wave_barrier();
-      f32x4 zc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+      f32x4 zc[2];
+      if constexpr (TAPS == 1) {
+        slab_gemm<2, BN>(ct, CS, w2s, W2S, W2R * W2S, fr, fg, zc);
+      } else {
+        f32x4 zm[4];
+        slab_gemm<4, BN>(ct, CS, w2s, W2S, W2R * W2S, fr, fg, zm);
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int kk = 0; kk < BN / 32; ++kk) {
-        const float* ap = ct + fr * CS + kk * 32 + fg * 8;
-        bf16x4 p0[2], p1[2];
-        split_planes<2>(*reinterpret_cast<const f4*>(ap), p0);
-        split_planes<2>(*reinterpret_cast<const f4*>(ap + 4), p1);
-        bf16x8 za[2];
+        for (int jn = 0; jn < 4; ++jn)
 #pragma unroll
-        for (int q = 0; q < 2; ++q)
-          za[q] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
-#pragma unroll
-        for (int jn = 0; jn < 2; ++jn) {
-          const uint16_t* bp = w2s + (jn * 16 + fr) * W2S + kk * 32 + fg * 8;
-          const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(bp);
-          const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(bp + 32 * W2S);
-          zc[jn] = mfma16(za[1], b0, zc[jn]);
-          zc[jn] = mfma16(za[0], b1, zc[jn]);
-          zc[jn] = mfma16(za[0], b0, zc[jn]);
-        }
+          for (int r = 0; r < 4; ++r)
+            ct[(fg * 4 + r) * CS + jn * 16 + fr] = apply_act(zm[jn][r] * s2[jn] + b2[jn], p.act2, 0.f);
+        __builtin_amdgcn_wave_barrier();
+        slab_gemm<2, 64>(ct, CS, w3s, W3S, 32 * W3S, fr, fg, zc);
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -312,7 +360,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   if (p.y_amax) amax_commit(p.y_amax + n, ym);
 }
 
-template <int NW, int TR, int TC, int TN, bool F16, bool APL, bool TAPS = false>
+template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0>
 int launch_halo(const ConvK& kp0, hipStream_t st) {
   ConvK kp = kp0;
   if (kp.w2 && kp.Co > TN * 16) return PRPE_EINVAL;     // the tap GEMM needs every column in one tile
@@ -333,10 +381,14 @@ int launch_halo_kind(const ConvK& kp, int prec, hipStream_t st) {
 }
 
 // epilogue tap GEMM: the 8 x 16-pixel, 128-column tile
+template <int TAPS>
+int launch_halo_taps_t(const ConvK& kp, int prec, hipStream_t st) {
+  if (prec == 3) return launch_halo<4, 8, 16, 8, true, false, TAPS>(kp, st);
+  return kp.x_planes ? launch_halo<4, 8, 16, 8, false, true, TAPS>(kp, st)
+                     : launch_halo<4, 8, 16, 8, false, false, TAPS>(kp, st);
+}
 int launch_halo_taps(const ConvK& kp, int prec, hipStream_t st) {
-  if (prec == 3) return launch_halo<4, 8, 16, 8, true, false, true>(kp, st);
-  return kp.x_planes ? launch_halo<4, 8, 16, 8, false, true, true>(kp, st)
-                     : launch_halo<4, 8, 16, 8, false, false, true>(kp, st);
+  return kp.w3 ? launch_halo_taps_t<2>(kp, prec, st) : launch_halo_taps_t<1>(kp, prec, st);
 }
 
 }  // namespace

@@ -642,6 +642,14 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
         d->y_planes || d->res_mode != PRPE_RES_NONE || d->y_amax || (uintptr_t)d->w2 % 16 || y.c % 4)
       return PRPE_EINVAL;
     kp.w2 = d->w2; kp.y2 = v2.ptr; kp.y2sn = v2.sn; kp.y2sh = v2.sh; kp.y2sw = v2.sw; kp.n2 = v2.c;
+    if (d->w3) {
+      if (d->n2 <= 0 || d->n2 > 64 || d->n2 % 4 || (uintptr_t)d->w3 % 16 || d->act2 < 0 || d->act2 > PRPE_ACT_SIGMOID ||
+          d->act2 == PRPE_ACT_PRELU)
+        return PRPE_EINVAL;
+      kp.w3 = d->w3; kp.s2 = d->scale2; kp.b2 = d->bias2; kp.act2 = d->act2; kp.nmid = d->n2;
+    }
+  } else if (d->w3) {
+    return PRPE_EINVAL;
   }
   kp.ylin = y.sh == (int64_t)Wo * y.sw && y.sn == (int64_t)Ho * y.sh;
   kp.rlin = d->res_mode == PRPE_RES_NONE ||

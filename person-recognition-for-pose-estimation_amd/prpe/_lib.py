@@ -36,7 +36,9 @@ class ConvDesc(C.Structure):
                 ("w_h16", C.c_void_p), ("w_l16", C.c_void_p), ("scale16", C.c_void_p),
                 ("x_amax", C.c_void_p), ("y_amax", C.c_void_p),
                 ("x2", View), ("x2_amax", C.c_void_p), ("x_planes", C.c_int32), ("y_planes", C.c_int32),
-                ("w2", C.c_void_p), ("y2", View)]
+                ("w2", C.c_void_p), ("y2", View),
+                ("w3", C.c_void_p), ("scale2", C.c_void_p), ("bias2", C.c_void_p), ("act2", C.c_int32),
+                ("n2", C.c_int32)]
 
 
 ACT = {"none": 0, "relu": 1, "silu": 2, "prelu": 3, "gelu": 4, "sigmoid": 5}

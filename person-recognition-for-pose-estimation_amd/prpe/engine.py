@@ -162,10 +162,11 @@ class Engine:
         return p
 
     def conv(self, x, p: ConvPack, out=None, res=None, res_mode=0, act=None, x2=None, x2_amax=None,
-             planes_out=False, w2=None, y2=None):
+             planes_out=False, w2=None, y2=None, **stage2):
         """``x2``: second 1x1 input on the output grid (dual-input GEMM, see prpe.h).
         ``planes_out``: the only consumer is a precision-0 wave-row conv: write the planes format.
-        ``w2``/``y2``: epilogue 1x1 GEMM into y2 (prpe.h); ``out`` is then not written."""
+        ``w2``/``y2``: epilogue 1x1 GEMM into y2 (prpe.h); ``out`` is then not written;
+        ``stage2``: its second stage (w3, scale2, bias2, act2; prpe.h)."""
         B, H, W, _ = x.shape
         Ho = (H + 2 * p.pad - p.kh) // p.stride + 1
         Wo = (W + 2 * p.pad - p.kw) // p.stride + 1
@@ -181,7 +182,8 @@ class Engine:
             raise RuntimeError(f"{p.name}: planes-format input needs precision 0, got {prec}")
         y_planes = PLANES_ON and planes_out and prec == 0 and p.co % 8 == 0 and out.is_contiguous()
         kw = dict(res=res, res_mode=res_mode, act=act, precision=prec, tile=p.tile, x_amax=xa, y_amax=ya, x2=x2,
-                  x2_amax=x2_amax if prec == 3 else None, x_planes=x_planes, y_planes=y_planes, w2=w2, y2=y2)
+                  x2_amax=x2_amax if prec == 3 else None, x_planes=x_planes, y_planes=y_planes, w2=w2, y2=y2,
+                  **stage2)
         if p.name in self.watch:          # HIP events around one kernel (bench roofline)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
@@ -386,11 +388,26 @@ class Engine:
                         act="silu", planes=True)
         t = self.conv(u, self.pk(a + ".7", a + ".7.weight", bn=a + ".8", bias_key=a + ".7.bias", act="silu"),
                       planes_out=True)
+        p10 = self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias", act="silu")
+        if SMALLCO_TAPS and TAPS_FUSE and getattr(t, "_prpe_planes", False):
+            # .10's epilogue runs .13 (1x1 128->64 + BN + SiLU) and .16's tap GEMM (64 -> 27):
+            # neither the 128- nor the 64-channel map reaches HBM (prpe.h, w2 / w3)
+            w2 = self.dev(a + ".13:w", lambda: self.sd[a + ".13.weight"].float().flatten(1))
+            s2 = self.dev(a + ".13:s", lambda: bn_affine(self.sd, a + ".14", BN_EPS, self.sd[a + ".13.bias"])[0])
+            b2 = self.dev(a + ".13:b", lambda: bn_affine(self.sd, a + ".14", BN_EPS, self.sd[a + ".13.bias"])[1])
+            w3 = self.dev(a + ".16:w2", lambda: self.sd[a + ".16.weight"].float().permute(2, 3, 0, 1)
+                          .reshape(-1, w2.shape[0]).contiguous())
+            B, H, W, _ = t.shape
+            z = self.empty(B, H, W, w3.shape[0])
+            sink = self.dev("sink:" + str(p10.co), lambda: torch.zeros(p10.co)).expand(B, H, W, p10.co)
+            self.conv(t, p10, out=sink, w2=w2, y2=z, w3=w3, scale2=s2, bias2=b2, act2="silu")
+            t = self.upconv(a + ".16", None, a + ".16.weight", (H, W), True, bn=a + ".17", bias_key=a + ".16.bias",
+                            act="silu", z=z)
+            return ops.norm_sigmoid(t, self.empty(*t.shape))
         # .10 and .13 write fp32: the 64-column 1x1 below runs faster on the register-staged
         # 256x64 tile than on the planes-input wave tile (1.12 vs 1.64 ms at bs=256), and the
         # 27-column tap GEMM after .13 needs fp32 input
-        t = self.conv(t, self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias",
-                                 act="silu"))
+        t = self.conv(t, p10)
         t = self.conv(t, self.pk(a + ".13", a + ".13.weight", bn=a + ".14", bias_key=a + ".13.bias", act="silu"))
         t = self.conv3x3_smallco(t, a + ".16", a + ".16.weight", bn=a + ".17", bias_key=a + ".16.bias",
                                  act="silu")

@@ -47,7 +47,8 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
 
 
 def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, tile=0, x_amax=None,
-           y_amax=None, x2=None, x2_amax=None, x_planes=False, y_planes=False, w2=None, y2=None):
+           y_amax=None, x2=None, x2_amax=None, x_planes=False, y_planes=False, w2=None, y2=None, w3=None,
+           scale2=None, bias2=None, act2="none"):
     """y = EPI(conv(PRO(x))) with a ``ConvPack`` (see prpe.pack).
 
     precision 3 (split fp16) needs ``x_amax``: a [N] device tensor, x_amax[n] bounding max|x[n]|
@@ -67,10 +68,17 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
     d.x_planes, d.y_planes = int(x_planes), int(y_planes)   # planes format, see prpe.h
     if w2 is not None:                 # epilogue 1x1 GEMM (w2 fp32 [n2][Co]) into y2, see prpe.h
         _gpu(w2, y2)
-        if w2.dtype != torch.float32 or not w2.is_contiguous() or w2.shape != (y2.shape[3], y.shape[3]):
+        n_mid = y2.shape[3] if w3 is None else w3.shape[1]
+        if w2.dtype != torch.float32 or not w2.is_contiguous() or w2.shape != (n_mid, y.shape[3]):
             raise ValueError(f"prpe_conv2d[{pack.name}]: w2 must be contiguous float32 [n2, Co]")
         d.w2 = w2.data_ptr()
         d.y2 = view(y2)
+        if w3 is not None:             # second stage: z1 = act2(scale2 (y' w2^T) + bias2), z = z1 w3^T
+            for t, shp in ((w3, (y2.shape[3], n_mid)), (scale2, (n_mid,)), (bias2, (n_mid,))):
+                if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.shape != shp):
+                    raise ValueError(f"prpe_conv2d[{pack.name}]: w3 [n3, n2] / scale2, bias2 [n2] float32")
+            d.w3, d.scale2, d.bias2 = w3.data_ptr(), _ptr(scale2), _ptr(bias2)
+            d.act2, d.n2 = ACT[act2], n_mid
     if x2 is not None:                 # second 1x1 input, see prpe.h (dual input)
         d.x2 = view(x2)
         d.x2_amax = _ptr(x2_amax)

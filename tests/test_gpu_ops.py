@@ -400,6 +400,54 @@ def test_conv_halo_taps_epilogue(B, Ci, H, W, Co, n2, mode):
         ops.conv2d(xd, pk, sink, w2=w2, y2=z, tile=28, **kw)
 
 
+@pytest.mark.parametrize("mode", ["fp32", "planes", "p3"])
+@pytest.mark.parametrize("B,Ci,H,W,Co,nmid,n3", [(2, 64, 17, 19, 128, 64, 27), (1, 96, 12, 35, 96, 40, 12)])
+def test_conv_halo_taps_two_stage(B, Ci, H, W, Co, nmid, n3, mode):
+    """prpe_conv_desc.w3: z1 = act2(scale2 (y' w2^T) + bias2) (w2 [nmid, Co]), then z = z1 w3^T
+    (w3 [n3, nmid]) in the haloed-tile kernel's epilogue (the YOLO adapter's .10 -> .13 -> .16
+    tap GEMM chain). Checked against fp64 of the same chain on the unfused conv output y', with
+    each stage's split-bf16 bound (2^-14 of its sum of |products|) carried through SiLU
+    (|silu'| <= 1.1)."""
+    x = rnd(B, Ci, H, W, seed=195)
+    if mode == "p3":
+        x = torch.relu(x) * 5.0
+    w = rnd(Co, Ci, 3, 3, seed=196, scale=1.0 / math.sqrt(Ci * 9))
+    sc = torch.rand(Co, generator=_g(197)) + 0.5
+    bi = rnd(Co, seed=198)
+    w2 = rnd(nmid, Co, seed=199, scale=1.0 / math.sqrt(Co)).to(DEV)
+    s2 = (torch.rand(nmid, generator=_g(200)) + 0.5).to(DEV)
+    b2 = rnd(nmid, seed=201).to(DEV)
+    w3 = rnd(n3, nmid, seed=202).to(DEV)
+    pk = pack.pack_conv("t", w, 1, 1, DEV, scale=sc, bias=bi, act="silu", k_order=1)
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    kw = dict(precision=0)
+    if mode == "planes":
+        xpl = torch.empty_like(xd)
+        ops.conv2d(xd, pack.pack_conv("i", torch.eye(Ci).view(Ci, Ci, 1, 1), 1, 0, DEV), xpl, precision=2,
+                   y_planes=True)
+        xd, kw = xpl, dict(precision=0, x_planes=True)
+    elif mode == "p3":
+        kw = dict(precision=3, x_amax=frame_amax(x).to(DEV))
+    y = torch.empty(B, H, W, Co, device=DEV)
+    ops.conv2d(xd, pk, y, tile=31, **kw)
+    sink = torch.full((B, H, W, Co), float("nan"), device=DEV)
+    z = torch.full((B, H, W, n3), float("nan"), device=DEV)
+    ops.conv2d(xd, pk, sink, w2=w2, y2=z, w3=w3, scale2=s2, bias2=b2, act2="silu", **kw)
+    torch.cuda.synchronize()
+    assert torch.isnan(sink).all()
+    yd = y.double().cpu()
+    w2d, w3d, s2d, b2d = (t.double().cpu() for t in (w2, w3, s2, b2))
+    u = (yd @ w2d.T) * s2d + b2d
+    z1 = u * torch.sigmoid(u)
+    ref = z1 @ w3d.T
+    e1 = 1.1 * s2d.abs() * (yd.abs() @ w2d.abs().T) * 2.0 ** -14 + z1.abs() * 2.0 ** -20
+    bound = (z1.abs() + e1) @ w3d.abs().T * 2.0 ** -14 + e1 @ w3d.abs().T
+    err = (z.double().cpu() - ref).abs()
+    assert torch.isfinite(z).all() and bool((err <= bound).all()), float((err / bound.clamp_min(1e-30)).max())
+    with pytest.raises(PrpeError):                    # PReLU has no slope vector in the second stage
+        ops.conv2d(xd, pk, sink, w2=w2, y2=z, w3=w3, scale2=s2, bias2=b2, act2="prelu", **kw)
+
+
 GEMM_SHAPES = [
     (2, 64, 13, 11, 256),       # M = 286: one full + one ragged 256-row tile, 2 K-steps
     (3, 768, 8, 12, 768),       # ViT-like: K = 768, three column tiles
