@@ -133,5 +133,7 @@ bool conv_halo_auto(const ConvK& kp, int prec);   // the automatic choice's shap
 bool conv_gemm_eligible(const ConvK& kp, int prec);
 int conv_gemm_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
+bool conv_splitk_eligible(const ConvK& kp, int prec, int k_order);
+int conv_splitk_launch(const ConvK& kp, hipStream_t st);
 
 }  // namespace prpe_k

@@ -672,6 +672,12 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   // direct fp32 kernel for tiny Co (needs the 3 weight planes; exact fp32 products); 1x1 only:
   // for 3x3 Co=3 the MFMA path measured faster (7.5 ms vs 11.8 ms at bs=256)
   const int khw = d->kh * d->kw;
+  // full-window linears with few M x N tiles (the IR-50 output layer): split along K
+  // (conv_splitk.hip); tile 50 forces it
+  if (tile == 50) return conv_splitk_eligible(kp, prec, d->k_order) ? conv_splitk_launch(kp, st) : PRPE_EINVAL;
+  if (tile == 0 && kp.K >= 4096 && (int64_t)((kp.M + 63) / 64) * (kp.Co / 64) < 256 &&
+      conv_splitk_eligible(kp, prec, d->k_order))
+    return conv_splitk_launch(kp, st);
   // epilogue 1x1 GEMM: the haloed-tile kernel's 128-column tile is the only implementation
   if (kp.w2) return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile ? tile : 31, st) : PRPE_EINVAL;
   if (tile == 0 && y.c <= 4 && km == 1 && !d->in_scale && d->w_lo && d->w_lo2 && x.c <= 256 && khw == 1) {

@@ -504,11 +504,14 @@ class Engine:
             w = sd[m + ".output_layer.3.weight"].float().view(512, 512, 7, 7)   # NCHW flatten order
             s1, b1 = bn_affine(sd, m + ".output_layer.4", BN_EPS, sd[m + ".output_layer.3.bias"])
             in_s, in_b = bn_affine(sd, m + ".output_layer.0", BN_EPS)
-            lin = pack_conv("ir50.output", w, 1, 0, self.device, scale=s1, bias=b1, in_scale=in_s, in_bias=in_b)
-            # M = frames (one output pixel each), K = 25,088: the automatic wave tile leaves 8
-            # blocks; the 128x16 register-staged tile runs 64 (bit-identical; PRPE_IR50_OUT_TILE=0
-            # restores the automatic choice; profiles/r01_conv_bench_ir50_output.txt)
-            lin.tile = int(os.environ.get("PRPE_IR50_OUT_TILE", "4"))
+            # M = frames (one output pixel each), K = 25,088: tap-major weights (k = the NHWC
+            # flatten order) for the automatic split-K path (conv_splitk.hip: one K-slice per tap,
+            # 392 workgroups at bs = 256); PRPE_IR50_OUT_TILE=4 runs the round-1 choice instead
+            # (the 128x16 register-staged tile, 64 blocks, chunk-major weights)
+            tile = int(os.environ.get("PRPE_IR50_OUT_TILE", "0"))
+            lin = pack_conv("ir50.output", w, 1, 0, self.device, scale=s1, bias=b1, in_scale=in_s, in_bias=in_b,
+                            k_order=0 if tile == 0 else "auto")
+            lin.tile = tile
             self._packs["ir50.output"] = lin
         B = x.shape[0]
         y = self.conv(x, lin)                                # [B,1,1,512]

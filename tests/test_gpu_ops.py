@@ -448,6 +448,27 @@ def test_conv_halo_taps_two_stage(B, Ci, H, W, Co, nmid, n3, mode):
         ops.conv2d(xd, pk, sink, w2=w2, y2=z, w3=w3, scale2=s2, bias2=b2, act2="prelu", **kw)
 
 
+@pytest.mark.parametrize("B,Ci,H,Co", [(5, 64, 7, 128), (70, 512, 7, 512), (3, 32, 4, 64), (2, 256, 2, 64)])
+def test_conv_splitk_linear(B, Ci, H, Co):
+    """conv_splitk.hip (full-window conv = linear over the flattened frame, split along K: the
+    IR-50 output layer): prologue BN, epilogue BN + PReLU, ragged frame counts; vs fp64 within
+    the precision-0 bound, and the automatic choice (tile 0) takes it for the IR-50 shape."""
+    x = rnd(B, Ci, H, H, seed=210)
+    w = rnd(Co, Ci, H, H, seed=211, scale=1.0 / math.sqrt(Ci * H * H))
+    sc = torch.rand(Co, generator=_g(212)) + 0.5
+    bi = rnd(Co, seed=213)
+    sl = torch.rand(Co, generator=_g(214)) * 0.3
+    ins = torch.rand(Ci, generator=_g(215)) + 0.5
+    inb = rnd(Ci, seed=216)
+    kw = dict(act="prelu", scale=sc, bias=bi, slope=sl, in_s=ins, in_b=inb, k_order=0)
+    got = run_conv(x, w, 1, 0, tile=50, **kw)
+    ref = ref_conv(x, w, 1, 0, act="prelu", scale=sc, bias=bi, slope=sl, in_s=ins, in_b=inb)
+    xs = x * ins.view(1, -1, 1, 1) + inb.view(1, -1, 1, 1)
+    torch.testing.assert_close(got, ref, rtol=0, atol=_tol(xs, w) * 2)
+    if Ci * H * H >= 4096:
+        assert torch.equal(run_conv(x, w, 1, 0, tile=0, **kw), got)
+
+
 GEMM_SHAPES = [
     (2, 64, 13, 11, 256),       # M = 286: one full + one ragged 256-row tile, 2 K-steps
     (3, 768, 8, 12, 768),       # ViT-like: K = 768, three column tiles

@@ -5,7 +5,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 TAG=${1:-model2}
 OFF=${2:-PRPE_CONV_GEMM}
-HIP_LAUNCH_BLOCKING=1 timeout -k 10 200 python -u -m pytest tests/test_gpu_ops.py -k "planes or attention or gemm or halo or upconv or smallco or activation" -x -q --timeout 100 --timeout-method thread > gpurun_out/${TAG}_newtests.log 2>&1 || { tail -40 gpurun_out/${TAG}_newtests.log; exit 1; }
+HIP_LAUNCH_BLOCKING=1 timeout -k 10 200 python -u -m pytest tests/test_gpu_ops.py -k "${KSEL:-planes or attention or gemm or halo or upconv or smallco or activation or splitk}" -x -q --timeout 100 --timeout-method thread > gpurun_out/${TAG}_newtests.log 2>&1 || { tail -40 gpurun_out/${TAG}_newtests.log; exit 1; }
 tail -1 gpurun_out/${TAG}_newtests.log
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/${TAG}_gputests.log 2>&1 || { tail -40 gpurun_out/${TAG}_gputests.log; exit 1; }
 tail -1 gpurun_out/${TAG}_gputests.log
