@@ -55,6 +55,8 @@ def main():
     ap.add_argument("--act", default="relu", help="epilogue activation (relu, gelu, silu, prelu, none)")
     ap.add_argument("--planes", action="store_true",
                     help="input in the planes format (x_planes; precision 0, wave-row kernel)")
+    ap.add_argument("--taps", type=int, default=0,
+                    help="epilogue 1x1 GEMM to this many channels (prpe_conv_desc.w2; y not written)")
     a = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -81,6 +83,9 @@ def main():
             for tile in [int(v) for v in a.tiles.split(",")]:
                 kw = dict(res=r, res_mode=1 if r is not None else 0, precision=prec, tile=tile, y_amax=ya,
                           x_amax=xa if prec == 3 else None, x_planes=a.planes)
+                if a.taps:
+                    kw["w2"] = torch.rand(a.taps, Co, device=dev) - 0.5
+                    kw["y2"] = torch.empty(B, Ho, Wo, a.taps, device=dev)
                 try:
                     ops.conv2d(x, pk, y, **kw)
                 except Exception as ex:              # tile not eligible for this shape
