@@ -188,8 +188,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       wait_barrier<0>();
       if (kt + 1 < nk) issue_b(kt + 1, (kt + 1) & 1);
       if (c + 1 < nc) {
-        const int q = t * NW + wave;                    // this wave's halo share of chunk c+1
-        if (q < HQ) issue_halo(q, c + 1, (c + 1) & 1);
+        // this wave's halo share of chunk c+1 (more than 9 * NW pieces: several per tap)
+        for (int q = t * NW + wave; q < HQ; q += 9 * NW) issue_halo(q, c + 1, (c + 1) & 1);
       }
       const int kh = t / 3, kw = t - kh * 3;
       // A fragments: 8 channels (two 16-B slots) of the tap-shifted pixel
