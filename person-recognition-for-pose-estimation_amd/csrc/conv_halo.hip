@@ -81,12 +81,16 @@ __device__ __forceinline__ void stage_planes(const float* w, int rows, int cols,
 // wave's LDS slice) is multiplied by w2 [n2][Co] (split-bf16 MFMAs, w2 split into LDS once per
 // block) and z is written to y2 instead of y. TAPS 2: z1 = act2(s2 (y' w2^T) + b2) with w2
 // [nmid <= 64][Co] first, back into the slice, then z = z1 w3^T (see prpe.h, w2 / w3).
-template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0>
+// WN: waves along N (WN = 2: a 2 x 2 wave grid, wave tile 64 px x BN/2; the B fragments of a
+// K-step are read by 2 waves instead of 4: -20 % LDS reads per MFMA at 4 waves).
+template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0, int WN = 1>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void conv_halo_kernel(ConvK p, int tiles_w, int tiles_h) {
-  static_assert(TC % 16 == 0 && (TR * TC / 16) % NW == 0, "tile");
+  static_assert(TC % 16 == 0 && (TR * TC / 16) % (NW / WN) == 0 && TN % WN == 0, "tile");
   static_assert(!(F16 && APL), "planes input is precision 0");
+  static_assert(WN == 1 || WN == 2, "waves along N");
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
-  constexpr int TM = TR * TC / 16 / NW;                 // 16-pixel row blocks per wave
+  constexpr int TM = TR * TC / 16 / (NW / WN);          // 16-pixel row blocks per wave
+  constexpr int TNW = TN / WN;                          // 16-column tiles per wave
   constexpr int BN = TN * 16, NP = 2;
   constexpr int HW_ = TC + 2, HP = (TR + 2) * HW_;      // halo pixels
   constexpr int HQ = (HP + 7) / 8;                      // 1-KiB DMA pieces per halo
@@ -95,7 +99,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   constexpr int NB_TOT = NP * BN / 16;                  // 1-KiB pieces per B stage
   constexpr int IB = NB_TOT / NW;
   static_assert(NB_TOT % NW == 0, "B pieces per wave");
-  constexpr int CS = BN + 4;
+  constexpr int CS = BN / WN + 4;
   constexpr int EPI = NW * 16 * CS * 4;
   constexpr int MAIN = 2 * HALO + 2 * B_STAGE;
   // w2 (and w3) bf16 planes after the slabs
@@ -107,6 +111,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   unsigned char* const ring = lds + 2 * HALO;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fg = lane >> 4;
   int L = xcd_remap(blockIdx.x, p.nwg);
   const int tile_n = L % p.tiles_n;
@@ -164,15 +169,15 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   int hbase[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int rb = wave * TM + i;
+    const int rb = wm * TM + i;
     hbase[i] = (rb / (TC / 16)) * HW_ + (rb % (TC / 16)) * 16 + fr;
   }
 
-  f32x4 acc[TM][TN];
+  f32x4 acc[TM][TNW];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < TNW; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nc = p.Ci / HBK;
   const int nk = nc * 9;
@@ -224,8 +229,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       }
       const unsigned char* sb = ring + (kt & 1) * B_STAGE;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int nrow = j * 16 + fr;
+      for (int j = 0; j < TNW; ++j) {
+        const int nrow = (wn * TNW + j) * 16 + fr;
         const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
         frag_t bfr[NP];
 #pragma unroll
@@ -243,11 +248,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 
   // ---------------- epilogue: per-wave 16-row slices (one row block = 16 consecutive pixels)
   float* ct = reinterpret_cast<float*>(lds) + wave * 16 * CS;
-  constexpr int CPR = BN / 4;
+  constexpr int CPR = BN / WN / 4;                     // this wave's columns: wn * BN / WN ..
   constexpr int RPP = 64 / CPR;
   constexpr int EB = 16 / RPP;
   const int cc = lane % CPR, rr0 = lane / CPR;
-  const int col = n0 + cc * 4;
+  const int col = n0 + wn * (BN / WN) + cc * 4;
   const bool cval = col < p.Co;
   f4 sc4 = {1.f, 1.f, 1.f, 1.f}, bi4 = {0.f, 0.f, 0.f, 0.f}, sl4 = {0.f, 0.f, 0.f, 0.f};
   if (cval) {
@@ -279,12 +284,12 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int rb = wave * TM + i;
+    const int rb = wm * TM + i;
     const int oh = oh0 + rb / (TC / 16), owb = ow0 + (rb % (TC / 16)) * 16;
 #pragma unroll
     for (int r = 0; r < 4; ++r)
 #pragma unroll
-      for (int j = 0; j < TN; ++j) ct[(fg * 4 + r) * CS + j * 16 + fr] = acc[i][j][r];
+      for (int j = 0; j < TNW; ++j) ct[(fg * 4 + r) * CS + j * 16 + fr] = acc[i][j][r];
     int64_t yo[EB];
     f4 res[EB];
     bool ok[EB];
@@ -327,40 +332,68 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     }
     if constexpr (TAPS != 0) {
       // z [16 pixels][32] = y' [16][BN] w2^T on the matrix cores, the two-plane (3-product)
-      // split as everywhere at precision 0: A = the activated slab rows, B = the w2 planes
+      // split as everywhere at precision 0: A = the activated slab rows, B = the w2 planes.
+      // WN = 2: each wave of a pair holds half of the rows' columns = half of this GEMM's K;
+      // the odd wave hands its partial sums to the even one through its slab (fixed order).
       __builtin_amdgcn_wave_barrier();
+      constexpr int KH = BN / WN;                     // this wave's share of K
+      const uint16_t* w2w = w2s + wn * KH;
+      auto hand_over = [&](auto& part, auto nt) {     // wn 1 -> wn 0: part[jn] += partner's
+        constexpr int NT_ = decltype(nt)::value;
+        if (wn == 1) {
+#pragma unroll
+          for (int jn = 0; jn < NT_; ++jn)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) ct[(fg * 4 + r) * CS + jn * 16 + fr] = part[jn][r];
+        }
+        __syncthreads();
+        if (wn == 0) {
+          const float* pc = ct + 16 * CS;             // the partner's slab (wave + 1)
+#pragma unroll
+          for (int jn = 0; jn < NT_; ++jn)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[jn][r] += pc[(fg * 4 + r) * CS + jn * 16 + fr];
+        }
+      };
       f32x4 zc[2];
       if constexpr (TAPS == 1) {
-        slab_gemm<2, BN>(ct, CS, w2s, W2S, W2R * W2S, fr, fg, zc);
+        slab_gemm<2, KH>(ct, CS, w2w, W2S, W2R * W2S, fr, fg, zc);
+        if constexpr (WN == 2) hand_over(zc, std::integral_constant<int, 2>{});
       } else {
         f32x4 zm[4];
-        slab_gemm<4, BN>(ct, CS, w2s, W2S, W2R * W2S, fr, fg, zm);
+        slab_gemm<4, KH>(ct, CS, w2w, W2S, W2R * W2S, fr, fg, zm);
+        if constexpr (WN == 2) hand_over(zm, std::integral_constant<int, 4>{});
         __builtin_amdgcn_wave_barrier();
+        if (wn == 0) {
 #pragma unroll
-        for (int jn = 0; jn < 4; ++jn)
+          for (int jn = 0; jn < 4; ++jn)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            ct[(fg * 4 + r) * CS + jn * 16 + fr] = apply_act(zm[jn][r] * s2[jn] + b2[jn], p.act2, 0.f);
-        __builtin_amdgcn_wave_barrier();
-        slab_gemm<2, 64>(ct, CS, w3s, W3S, 32 * W3S, fr, fg, zc);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int ow = owb + fg * 4 + r;
-        if (oh < p.Ho && ow < p.Wo) {
-          float* zo = p.y2 + (int64_t)n * p.y2sn + (int64_t)oh * p.y2sh + (int64_t)ow * p.y2sw;
-#pragma unroll
-          for (int jn = 0; jn < 2; ++jn)
-            if (jn * 16 + fr < p.n2) zo[jn * 16 + fr] = zc[jn][r];
+            for (int r = 0; r < 4; ++r)
+              ct[(fg * 4 + r) * CS + jn * 16 + fr] = apply_act(zm[jn][r] * s2[jn] + b2[jn], p.act2, 0.f);
+          __builtin_amdgcn_wave_barrier();
+          slab_gemm<2, 64>(ct, CS, w3s, W3S, 32 * W3S, fr, fg, zc);
         }
       }
+      if (wn == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ow = owb + fg * 4 + r;
+          if (oh < p.Ho && ow < p.Wo) {
+            float* zo = p.y2 + (int64_t)n * p.y2sn + (int64_t)oh * p.y2sh + (int64_t)ow * p.y2sw;
+#pragma unroll
+            for (int jn = 0; jn < 2; ++jn)
+              if (jn * 16 + fr < p.n2) zo[jn * 16 + fr] = zc[jn][r];
+          }
+        }
+      }
+      if constexpr (WN == 2) __syncthreads();       // the slabs are rewritten by the next row block
       __builtin_amdgcn_wave_barrier();
     }
   }
   if (p.y_amax) amax_commit(p.y_amax + n, ym);
 }
 
-template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0>
+template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0, int WN = 1>
 int launch_halo(const ConvK& kp0, hipStream_t st) {
   ConvK kp = kp0;
   if (kp.w2 && kp.Co > TN * 16) return PRPE_EINVAL;     // the tap GEMM needs every column in one tile
@@ -369,26 +402,40 @@ int launch_halo(const ConvK& kp0, hipStream_t st) {
   const int64_t nwg = (int64_t)(kp.M / kp.HoWo) * tiles_h * tiles_w * kp.tiles_n;
   if (nwg <= 0 || nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
-  hipLaunchKernelGGL((conv_halo_kernel<NW, TR, TC, TN, F16, APL, TAPS>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp,
+  hipLaunchKernelGGL((conv_halo_kernel<NW, TR, TC, TN, F16, APL, TAPS, WN>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp,
                      tiles_w, tiles_h);
   return launch_status();
 }
 
-template <int NW, int TR, int TC, int TN>
+template <int NW, int TR, int TC, int TN, int WN = 1>
 int launch_halo_kind(const ConvK& kp, int prec, hipStream_t st) {
-  if (prec == 3) return launch_halo<NW, TR, TC, TN, true, false>(kp, st);
-  return kp.x_planes ? launch_halo<NW, TR, TC, TN, false, true>(kp, st) : launch_halo<NW, TR, TC, TN, false, false>(kp, st);
+  if (prec == 3) return launch_halo<NW, TR, TC, TN, true, false, 0, WN>(kp, st);
+  return kp.x_planes ? launch_halo<NW, TR, TC, TN, false, true, 0, WN>(kp, st)
+                     : launch_halo<NW, TR, TC, TN, false, false, 0, WN>(kp, st);
 }
 
 // epilogue tap GEMM: the 8 x 16-pixel, 128-column tile
-template <int TAPS>
+template <int TAPS, int WN>
 int launch_halo_taps_t(const ConvK& kp, int prec, hipStream_t st) {
-  if (prec == 3) return launch_halo<4, 8, 16, 8, true, false, TAPS>(kp, st);
-  return kp.x_planes ? launch_halo<4, 8, 16, 8, false, true, TAPS>(kp, st)
-                     : launch_halo<4, 8, 16, 8, false, false, TAPS>(kp, st);
+  if (prec == 3) return launch_halo<4, 8, 16, 8, true, false, TAPS, WN>(kp, st);
+  return kp.x_planes ? launch_halo<4, 8, 16, 8, false, true, TAPS, WN>(kp, st)
+                     : launch_halo<4, 8, 16, 8, false, false, TAPS, WN>(kp, st);
+}
+// PRPE_HALO_WN=2: the 2 x 2 wave grid (WN = 2) for the automatic and epilogue-GEMM tiles.
+// Off by default: in the model at bs = 256 it measured ViT adapter.7 +0.6 %, face-YOLO .10
+// +2.8 % (two block barriers per row block in the chain epilogue), AdaFace .7 -2.8 %, bench
+// 1363 -> 1357 frames/s (profiles/r02_layer_profile_halo_wn.txt), although the micro-bench on
+// random data had it 4-12 % faster (profiles/r02_conv_bench_halo_wn.txt).
+int halo_wn() {
+  static const int wn = [] {
+    const char* e = getenv("PRPE_HALO_WN");
+    return e && e[0] == '2' ? 2 : 1;
+  }();
+  return wn;
 }
 int launch_halo_taps(const ConvK& kp, int prec, hipStream_t st) {
-  return kp.w3 ? launch_halo_taps_t<2>(kp, prec, st) : launch_halo_taps_t<1>(kp, prec, st);
+  if (halo_wn() == 2) return kp.w3 ? launch_halo_taps_t<2, 2>(kp, prec, st) : launch_halo_taps_t<1, 2>(kp, prec, st);
+  return kp.w3 ? launch_halo_taps_t<2, 1>(kp, prec, st) : launch_halo_taps_t<1, 1>(kp, prec, st);
 }
 
 }  // namespace
@@ -419,13 +466,15 @@ bool conv_halo_auto(const ConvK& kp, int prec) {
 // 31..35 force a configuration
 int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
   if (kp.w2) return tile == 30 || tile == 31 ? launch_halo_taps(kp, prec, st) : PRPE_EINVAL;
-  if (tile == 30) tile = kp.Co <= 64 ? 34 : 31;
+  if (tile == 30) tile = kp.Co <= 64 ? 34 : (halo_wn() == 2 ? 36 : 31);
   switch (tile) {
     case 31: return launch_halo_kind<4, 8, 16, 8>(kp, prec, st);     // 8 x 16 px, 4 waves, 128 ch
     case 32: return launch_halo_kind<8, 16, 16, 8>(kp, prec, st);    // 16 x 16 px, 8 waves, 128 ch
     case 33: return launch_halo_kind<8, 8, 32, 8>(kp, prec, st);     // 8 x 32 px, 8 waves, 128 ch
     case 34: return launch_halo_kind<4, 8, 16, 4>(kp, prec, st);     // 8 x 16 px, 4 waves, 64 ch
     case 35: return launch_halo_kind<8, 16, 16, 4>(kp, prec, st);    // 16 x 16 px, 8 waves, 64 ch
+    case 36: return launch_halo_kind<4, 8, 16, 8, 2>(kp, prec, st);  // 8 x 16 px, 2 x 2 waves (64 px x 64 ch), 128 ch
+    case 37: return launch_halo_kind<8, 16, 16, 8, 2>(kp, prec, st); // 16 x 16 px, 4 x 2 waves (64 px x 64 ch), 128 ch
     default: return PRPE_EINVAL;
   }
 }

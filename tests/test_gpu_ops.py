@@ -312,7 +312,7 @@ HALO_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("tile", [30, 31, 32, 33, 34, 35])
+@pytest.mark.parametrize("tile", [30, 31, 32, 33, 34, 35, 36, 37])
 @pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", HALO_SHAPES)
 def test_conv_halo_kernel_bit_exact_vs_wave(B, Ci, H, W, Co, k, s, p, tile):
     """conv_halo.hip (input patch + halo staged once per 32-channel chunk, A fragments of every

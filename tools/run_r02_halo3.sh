@@ -4,7 +4,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 TAG=${1:-halo3}
-TILES=${TILES:-31,36}
+TILES=${TILES:-31,36,32,37}
 HIP_LAUNCH_BLOCKING=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -k "halo" -x -q --timeout 200 --timeout-method thread > gpurun_out/${TAG}_tests.log 2>&1 || { tail -40 gpurun_out/${TAG}_tests.log; exit 1; }
 tail -1 gpurun_out/${TAG}_tests.log
 : > gpurun_out/${TAG}_cb.txt
