@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--precision", type=int, required=True)
     ap.add_argument("--algorithmic", type=float, required=True, help="algorithmic HBM bytes per launch")
     ap.add_argument("--shape", default="")
+    ap.add_argument("--command", default="tools/run_r02_final.sh")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     import bench
@@ -55,7 +56,7 @@ def main():
            "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
            "algorithmic_bytes_per_launch": a.algorithmic, "avg_us_profiled": [round(tf, 1), round(tw, 1)],
            "sources_sha": bench.kernel_sources_hash(),
-           "command": "tools/run_r02_final.sh (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, separate passes)"}
+           "command": f"{a.command} (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, separate passes)"}
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out))
 
