@@ -8,8 +8,8 @@ Configs (BASELINE.json ``configs``; the bench line is config 4 by default):
   full       config 4 (config 5 at N = 8): 256 synthetic 640x640 frames per GPU, resident in
              HBM; ResNet-50 trunk once -> face-YOLO (det [B,5,525], strides 8/16/32) + AdaFace
              (emb, norm) + ViTPose-B (heatmaps) -> batched NMS (padded, on device) + heatmap
-             soft-argmax; for N > 1 the per-rank padded detections are all-gathered over RCCL
-             (the only exchange).
+             soft-argmax; for N > 1 the per-rank frame records (padded detections, embeddings,
+             keypoints) are all-gathered over RCCL (the only exchange).
   yolo_face  config 2: 64 frames per GPU, trunk -> face-YOLO -> NMS.
   vitpose    config 3: 256 pixel_values crops [3,256,192] per GPU -> ViTPose-B -> soft-argmax.
 Frames shard across ranks (each rank owns a contiguous slice of the global batch), weights are
@@ -35,6 +35,8 @@ Rank 0 prints ONE JSON line. Extra objects:
   parity       — the GPU outputs vs that CPU reference on frames spread over the batch
                  (0, B/3, 2B/3, B-1): heatmaps / embeddings max|d|, keypoint OKS delta (max
                  over the sampled frames), NMS exactness on the sampled frames.
+For N > 1 the full config all-gathers each frame's record (padded detections + count,
+embedding + norm, keypoints + scores: 9.5 KB per frame) in one collective per step.
 """
 from __future__ import annotations
 
@@ -168,7 +170,7 @@ def main():
         observed_ws = 1
 
     from prpe import CombinedModel, arch, ops, synth
-    from prpe.dist import gather_detections, gather_tensor
+    from prpe.dist import gather_detections, gather_frame_records, gather_tensor
     from prpe.postproc import non_max_suppression_padded
 
     cfg = args.config
@@ -192,7 +194,9 @@ def main():
             coords, scores = ops.softargmax(o["heatmaps"])
             o.update(dets=dets, cnt=cnt, coords=coords)
             if ws > 1:
-                gather_detections(dets, cnt)          # RCCL all-gather over xGMI (prpe/dist.py)
+                # one RCCL all-gather over xGMI of each frame's record: detections + count,
+                # embedding + norm, keypoints + scores (prpe/dist.py)
+                gather_frame_records([dets, cnt, o["emb"], o["norm"], torch.cat([coords, scores[..., None]], -1)])
         elif cfg == "yolo_face":
             det = eng.yolo("yolo_face", eng.trunk(x), STRIDE)
             dets, cnt = non_max_suppression_padded(det)

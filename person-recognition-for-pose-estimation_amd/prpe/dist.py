@@ -55,3 +55,27 @@ def gather_tensor(t: torch.Tensor, global_batch: int | None = None, group=None) 
 def gather_detections(dets: torch.Tensor, counts: torch.Tensor, global_batch: int | None = None, group=None):
     """All-gather per-rank (dets [b,D,6], counts [b]) -> ([B_global,D,6], [B_global])."""
     return gather_tensor(dets, global_batch, group), gather_tensor(counts, global_batch, group)
+
+
+def gather_frame_records(parts, global_batch: int | None = None, group=None):
+    """All-gather several per-frame tensors in ONE collective (xGMI is point-to-point: one
+    larger all-gather instead of one per tensor). ``parts``: tensors [b, ...] of float32 or
+    int32 (bit-cast into the fp32 record, so integers travel exactly); returns the gathered
+    tensors [B_global, ...] with their dtypes and shapes. SURVEY.md §8e: detections + counts,
+    optionally embeddings [b,512] and keypoints + scores [b,17,3] (~9.5 KB per frame)."""
+    if dist.get_world_size(group) == 1:
+        return list(parts)
+    b = parts[0].shape[0]
+    flat = []
+    for t in parts:
+        if t.shape[0] != b or t.dtype not in (torch.float32, torch.int32):
+            raise ValueError("gather_frame_records: [b, ...] float32 / int32 tensors of one batch")
+        flat.append(t.contiguous().view(torch.float32).reshape(b, -1))
+    rec = gather_tensor(torch.cat(flat, 1), global_batch, group)
+    out, o = [], 0
+    for t, f in zip(parts, flat):
+        w = f.shape[1]
+        out.append(rec[:, o:o + w].contiguous().view(t.dtype).reshape((rec.shape[0],) + tuple(t.shape[1:])))
+        o += w
+    return out
+

@@ -10,7 +10,7 @@ import torch.distributed as dist
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                 "person-recognition-for-pose-estimation_amd"))
-from prpe.dist import gather_detections, shard_range  # noqa: E402
+from prpe.dist import gather_detections, gather_frame_records, shard_range  # noqa: E402
 
 
 def main():
@@ -26,7 +26,14 @@ def main():
             dets[i, :f % 3] = float(f)
         ragged = gb % world != 0
         gd, gc = gather_detections(dets, cnt, global_batch=gb if ragged else None)
-        torch.save({"gd": gd, "gc": gc, "rank": rank, "world": world,
+        # one-collective record: detections, counts, an int32 id that needs exact bits,
+        # embeddings and keypoints (bench.py's full config over RCCL)
+        fr = torch.arange(s, e)
+        ids = (fr * 1000003 + 7).to(torch.int32)
+        emb = fr[:, None].float() + torch.arange(512).float()[None] * 1e-3
+        kp = fr[:, None, None].float() * 0.5 + torch.zeros(e - s, 17, 3)
+        rec = gather_frame_records([dets, cnt, ids, emb, kp], global_batch=gb if ragged else None)
+        torch.save({"gd": gd, "gc": gc, "rec": rec, "rank": rank, "world": world,
                     "local_rank": int(os.environ.get("LOCAL_RANK", "-1"))}, f"{out}.{rank}")
     finally:
         dist.destroy_process_group()

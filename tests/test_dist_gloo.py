@@ -1,4 +1,5 @@
-"""CPU: the N > 1 path (frame sharding + all-gather of padded detections) over gloo, exactly
+"""CPU: the N > 1 path (frame sharding + all-gather of padded detections, and the one-collective
+per-frame record of detections + counts + embeddings + keypoints) over gloo, exactly
 the logic bench.py runs over RCCL, at world sizes 2 and 4 (even and ragged global batches),
 and bench.py's own launcher (one child per rank, rendezvous env on 127.0.0.1)."""
 import os
@@ -40,6 +41,12 @@ def _check(out, world, gb):
         assert gd.shape == (gb, 300, 6) and gc.tolist() == [f % 3 for f in range(gb)]
         for f in range(gb):
             assert torch.all(gd[f, :f % 3] == f) and torch.all(gd[f, f % 3:] == 0)
+        rd, rc, ids, emb, kp = res["rec"]
+        fr = torch.arange(gb)
+        assert torch.equal(rd, gd) and torch.equal(rc, gc) and rc.dtype == torch.int32
+        assert ids.dtype == torch.int32 and torch.equal(ids, (fr * 1000003 + 7).to(torch.int32))
+        assert emb.shape == (gb, 512) and torch.equal(emb, fr[:, None].float() + torch.arange(512).float()[None] * 1e-3)
+        assert kp.shape == (gb, 17, 3) and torch.equal(kp, fr[:, None, None].float() * 0.5 + torch.zeros(gb, 17, 3))
 
 
 @pytest.mark.parametrize("world,gb", [(2, 6), (4, 7)])
