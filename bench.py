@@ -27,8 +27,9 @@ Rank 0 prints ONE JSON line. Extra objects:
                  its in-region, co-resident time is reported beside it); achieved = its
                  algorithmic FLOPs per launch / mean launch time; peak = dense bf16 MFMA 2.5 PF/s.
                  ``traffic`` (HBM bytes per launch, PMC FETCH_SIZE x2 + WRITE_SIZE) comes from the
-                 committed profiles/r02_pmc_traffic_<config>.json only while the kernel sources
-                 hash to the value recorded there (else null, "stale").
+                 committed profiles/r02_pmc_traffic_<config>.json only while the sources of that
+                 kernel (the files listed there) hash to the value recorded there (else null,
+                 "stale").
   cpu_baseline — the oracle (fp32 PyTorch-CPU restatement of the reference, pinned against the
                  reference itself) on this host's usable cores: warm-up 1, median of 5, at
                  bs=1 and bs=8 (value = the bs=8 rate). A reported baseline, not the target.
@@ -133,10 +134,15 @@ def usable_cores() -> int:
     return max(1, n)
 
 
-def kernel_sources_hash() -> str:
+def kernel_sources_hash(names=None) -> str:
+    """Hash of the kernel sources (csrc/*.hip, *.h), or of just ``names`` (the files the
+    measured kernel is built from, e.g. ["conv_halo.hip", "conv.h", "common.h"])."""
     h = hashlib.sha256()
     pkg = os.path.join(ROOT, "person-recognition-for-pose-estimation_amd", "csrc")
-    for f in sorted(glob.glob(os.path.join(pkg, "*.hip")) + glob.glob(os.path.join(pkg, "*.h"))):
+    files = sorted(glob.glob(os.path.join(pkg, "*.hip")) + glob.glob(os.path.join(pkg, "*.h")))
+    if names:
+        files = sorted(os.path.join(pkg, n) for n in names)
+    for f in files:
         h.update(open(f, "rb").read())
     return h.hexdigest()[:16]
 
@@ -273,7 +279,7 @@ def main():
         tp = os.path.join(ROOT, "profiles", f"r02_pmc_traffic_{cfg}.json")
         if os.path.exists(tp):
             t = json.load(open(tp))
-            fresh = (t.get("sources_sha") == kernel_sources_hash() and t.get("batch") == B
+            fresh = (t.get("sources_sha") == kernel_sources_hash(t.get("sources")) and t.get("batch") == B
                      and t.get("layer") in dominant and t.get("precision") == precn)
             if fresh:
                 roof["traffic"] = round(t["hbm_bytes_per_launch"] / 1e9, 3)

@@ -17,6 +17,16 @@ __device__ __forceinline__ int64_t voff(const prpe_view& v, int n, int h, int w,
   return (int64_t)n * v.sn + (int64_t)h * v.sh + (int64_t)w * v.sw + (int64_t)c * v.sc;
 }
 
+// x + (1 - l) a + l b with one fixed rounding sequence (fma((1 - l), a, l * b), then the add):
+// every upconv form (fused, producer / consumer, separable) evaluates it identically whatever
+// FP contraction the surrounding code would allow
+__device__ __forceinline__ float lerp_add(float x, float l, float a, float b) {
+  const float t = __builtin_fmaf(1.f - l, a, l * b);
+  float r;
+  asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(t));
+  return r;
+}
+
 // PyTorch upsample_bilinear2d source index (aten/src/ATen/native/UpSample.h semantics):
 // align_corners: src = dst * (in-1)/(out-1); else src = max(0, (dst+0.5)*in/out - 0.5).
 __device__ __forceinline__ void bilin_src(int dst, int in, int out, int ac, int& i0, int& i1, float& l1) {
@@ -86,12 +96,12 @@ __device__ __forceinline__ void up_hrow(const float* __restrict__ zrow, const Up
     const float* b = zrow + ux[dx].o1;
     if constexpr (VW == 4) {
       const float4 A = *reinterpret_cast<const float4*>(a), B = *reinterpret_cast<const float4*>(b);
-      h[0] += (1.f - lx) * A.x + lx * B.x;
-      h[1] += (1.f - lx) * A.y + lx * B.y;
-      h[2] += (1.f - lx) * A.z + lx * B.z;
-      h[3] += (1.f - lx) * A.w + lx * B.w;
+      h[0] = lerp_add(h[0], lx, A.x, B.x);
+      h[1] = lerp_add(h[1], lx, A.y, B.y);
+      h[2] = lerp_add(h[2], lx, A.z, B.z);
+      h[3] = lerp_add(h[3], lx, A.w, B.w);
     } else {
-      h[0] += (1.f - lx) * a[0] + lx * b[0];
+      h[0] = lerp_add(h[0], lx, a[0], b[0]);
     }
   }
 }
@@ -188,7 +198,7 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
         cur[dy] = y0;
       }
 #pragma unroll
-      for (int v = 0; v < VW; ++v) acc[v] += (1.f - ly) * hA[dy][v] + ly * hB[dy][v];
+      for (int v = 0; v < VW; ++v) acc[v] = lerp_add(acc[v], ly, hA[dy][v], hB[dy][v]);
     }
     float out[VW];
 #pragma unroll
@@ -246,12 +256,12 @@ __global__ __launch_bounds__(256) void upconv_h_kernel(UpK p, float* __restrict_
     const float* b = z + (int64_t)x1 * p.z.sw;
     if constexpr (VW == 4) {
       const float4 A = *reinterpret_cast<const float4*>(a), B = *reinterpret_cast<const float4*>(b);
-      acc[0] += (1.f - lx) * A.x + lx * B.x;
-      acc[1] += (1.f - lx) * A.y + lx * B.y;
-      acc[2] += (1.f - lx) * A.z + lx * B.z;
-      acc[3] += (1.f - lx) * A.w + lx * B.w;
+      acc[0] = lerp_add(acc[0], lx, A.x, B.x);
+      acc[1] = lerp_add(acc[1], lx, A.y, B.y);
+      acc[2] = lerp_add(acc[2], lx, A.z, B.z);
+      acc[3] = lerp_add(acc[3], lx, A.w, B.w);
     } else {
-      acc[0] += (1.f - lx) * a[0] + lx * b[0];
+      acc[0] = lerp_add(acc[0], lx, a[0], b[0]);
     }
   }
   float* h = H + ((int64_t)row * Wo + ox) * p.Co + c0;
@@ -283,12 +293,12 @@ __global__ __launch_bounds__(256) void upconv_out_kernel(UpK p, const float* __r
     const float* b = hb + (int64_t)y1 * Wo * p.Co;
     if constexpr (VW == 4) {
       const float4 A = *reinterpret_cast<const float4*>(a), B = *reinterpret_cast<const float4*>(b);
-      acc[0] += (1.f - ly) * A.x + ly * B.x;
-      acc[1] += (1.f - ly) * A.y + ly * B.y;
-      acc[2] += (1.f - ly) * A.z + ly * B.z;
-      acc[3] += (1.f - ly) * A.w + ly * B.w;
+      acc[0] = lerp_add(acc[0], ly, A.x, B.x);
+      acc[1] = lerp_add(acc[1], ly, A.y, B.y);
+      acc[2] = lerp_add(acc[2], ly, A.z, B.z);
+      acc[3] = lerp_add(acc[3], ly, A.w, B.w);
     } else {
-      acc[0] += (1.f - ly) * a[0] + ly * b[0];
+      acc[0] = lerp_add(acc[0], ly, a[0], b[0]);
     }
   }
   float out[VW];

@@ -880,9 +880,10 @@ def test_epilogue_activation_accuracy(act):
                                         (20, 20, 112, 112, True), (9, 5, 40, 17, False), (13, 6, 37, 11, True),
                                         (20, 7, 51, 9, False), (11, 4, 61, 8, True)])
 def test_upconv_fused_matches_separable(hi, wi, ho, wo, ac):
-    """The one-pass rolling-row kernel and the two-pass separable form evaluate the same sum
-    (FMA contraction may differ: fp32-rounding-level agreement), at the adapters' upsampling
-    ratios and at awkward ones (source intervals of 1-2 output rows, both align_corners modes)."""
+    """The one-pass rolling-row kernel and the two-pass separable form evaluate the same sum in
+    the same rounding sequence (pointwise.hip lerp_add): bit-identical, at the adapters'
+    upsampling ratios and at awkward ones (source intervals of 1-2 output rows, both
+    align_corners modes)."""
     Co = 24
     z = rnd(2, hi, wi, 9 * Co, seed=103).to(DEV)
     sc = (torch.rand(Co, generator=_g(104)) + 0.5).to(DEV)
@@ -892,7 +893,7 @@ def test_upconv_fused_matches_separable(hi, wi, ho, wo, ac):
         y = torch.empty(2, ho, wo, Co, device=DEV)
         ops.upconv3x3(z, y, ac, sc, bi, None, "gelu", separable=sep)
         outs.append(y.cpu())
-    torch.testing.assert_close(outs[0], outs[1], rtol=1e-6, atol=1e-6)
+    assert torch.equal(outs[0], outs[1])
 
 
 def test_upconv_nchw_output_view():

@@ -24,7 +24,7 @@ done
 # algorithmic bytes: planes input 256 x 256 x 192 x 256 x 4 B + the epilogue tap GEMM's fp32
 # output (27 ch; the 128-ch map stays in LDS) + weight planes (3x3 x 256 x 128 x 2 x 2 B)
 python tools/traffic_json.py gpurun_out/${TAG}_tr_FETCH_SIZE gpurun_out/${TAG}_tr_WRITE_SIZE --kernel conv_halo --min-us 5000 \
-  --layer vit_pose.adapter.7 --batch 256 --precision 0 --algorithmic 14245036032 \
+  --layer vit_pose.adapter.7 --batch 256 --precision 0 --algorithmic 14245036032 --sources conv_halo.hip,conv.h,common.h \
   --shape "3x3 256->128 @256x192, planes input, GELU, epilogue tap GEMM to 27 ch" --out gpurun_out/r02_pmc_traffic_full.json
 rm -rf gpurun_out/${TAG}_tr_FETCH_SIZE gpurun_out/${TAG}_tr_WRITE_SIZE
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_bench -o bench -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err || { tail -20 gpurun_out/${TAG}_bench.err; exit 1; }

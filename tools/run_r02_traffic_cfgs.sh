@@ -14,11 +14,11 @@ done
 # algorithmic bytes -- yolo_face.adapter.10 at bs 64: planes input 64*160*160*256*4 + the chain's
 # 27-channel fp32 output 64*160*160*27*4 + weight planes 9*256*128*2*2 (+ w2 / w3, < 0.1 MB)
 python tools/traffic_json.py gpurun_out/yf_FETCH_SIZE gpurun_out/yf_WRITE_SIZE --kernel "conv_halo_kernel<4, 8, 16, 8, false, true, 2" --min-us 1000 \
-  --layer yolo_face.adapter.10 --batch 64 --precision 0 --algorithmic 1855848448 \
+  --layer yolo_face.adapter.10 --batch 64 --precision 0 --algorithmic 1855848448 --sources conv_halo.hip,conv.h,common.h \
   --shape "3x3 256->128 @160x160, planes input, SiLU, epilogue chain 1x1 128->64 + SiLU -> 27 taps" --out gpurun_out/r02_pmc_traffic_yolo_face.json --command tools/run_r02_traffic_cfgs.sh
 # vit fc1 at 256 crops: planes input 49152*768*4 + planes output 49152*3072*4 + weight planes 3072*768*2*2
 python tools/traffic_json.py gpurun_out/vp_FETCH_SIZE gpurun_out/vp_WRITE_SIZE --kernel conv_gemm_kernel --min-us 300 \
-  --layer "vit_pose.vit_pose.backbone.encoder.layer.0:fc1" --batch 256 --precision 0 --algorithmic 764411904 \
+  --layer "vit_pose.vit_pose.backbone.encoder.layer.0:fc1" --batch 256 --precision 0 --algorithmic 764411904 --sources conv_gemm.hip,conv.h,common.h \
   --shape "1x1 768->3072 over 49152 tokens, planes input and output, GELU" --out gpurun_out/r02_pmc_traffic_vitpose.json --command tools/run_r02_traffic_cfgs.sh
 rm -rf gpurun_out/yf_FETCH_SIZE gpurun_out/yf_WRITE_SIZE gpurun_out/vp_FETCH_SIZE gpurun_out/vp_WRITE_SIZE
 cat gpurun_out/r02_pmc_traffic_yolo_face.json gpurun_out/r02_pmc_traffic_vitpose.json

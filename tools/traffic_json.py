@@ -44,18 +44,20 @@ def main():
     ap.add_argument("--algorithmic", type=float, required=True, help="algorithmic HBM bytes per launch")
     ap.add_argument("--shape", default="")
     ap.add_argument("--command", default="tools/run_r02_final.sh")
+    ap.add_argument("--sources", default="", help="comma list of the csrc files the kernel is built from")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
     import bench
     f, tf, name = avg_counter(a.fetch_dir, "FETCH_SIZE", a.kernel, a.min_us)
     w, tw, _ = avg_counter(a.write_dir, "WRITE_SIZE", a.kernel, a.min_us)
     rd, wr = f * 2 * 1024, w * 1024
+    srcs = [x for x in a.sources.split(",") if x] or None
     out = {"kernel": name[:160], "layer": a.layer, "shape": a.shape, "batch": a.batch, "precision": a.precision,
            "fetch_size_kib": f, "write_size_kib": w,
            "correction": "FETCH_SIZE x2 (gfx950: half the bytes of 16-B-per-lane reads); WRITE_SIZE as reported",
            "hbm_read_bytes": rd, "hbm_write_bytes": wr, "hbm_bytes_per_launch": rd + wr,
            "algorithmic_bytes_per_launch": a.algorithmic, "avg_us_profiled": [round(tf, 1), round(tw, 1)],
-           "sources_sha": bench.kernel_sources_hash(),
+           "sources": srcs, "sources_sha": bench.kernel_sources_hash(srcs),
            "command": f"{a.command} (rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE --kernel-trace, separate passes)"}
     json.dump(out, open(a.out, "w"), indent=1)
     print(json.dumps(out))
