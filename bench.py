@@ -202,7 +202,8 @@ def main():
             if ws > 1:
                 # one RCCL all-gather over xGMI of each frame's record: detections + count,
                 # embedding + norm, keypoints + scores (prpe/dist.py)
-                gather_frame_records([dets, cnt, o["emb"], o["norm"], torch.cat([coords, scores[..., None]], -1)])
+                o["gathered"] = gather_frame_records([dets, cnt, o["emb"], o["norm"],
+                                                      torch.cat([coords, scores[..., None]], -1)])
         elif cfg == "yolo_face":
             det = eng.yolo("yolo_face", eng.trunk(x), STRIDE)
             dets, cnt = non_max_suppression_padded(det)
@@ -293,6 +294,18 @@ def main():
     cpu = parity = None
     if rank == 0 and not args.no_cpu_baseline and ws == 1:
         parity, cpu = cpu_legs(cfg, sd, x, o, B, args.cpu_reps)
+    # ---- N > 1 (full config): rank 0 checks the records the timed region's all-gather delivered
+    # for sampled frames of EVERY rank's shard against the oracle on those frames (regenerated
+    # from the rank's input seed); each rank contributes its sampled frames' raw det rows (one
+    # more small all-gather, outside the timed region) so NMS exactness is checked on them
+    if ws > 1 and cfg == "full" and not args.no_cpu_baseline:
+        det_samples = gather_tensor(o["det"][sample_local(B)].contiguous())
+        if rank == 0:
+            from oracle import model_ref as R
+            torch.set_num_threads(usable_cores())
+            recs = [t.cpu() for t in o["gathered"]]
+            parity = gathered_parity(recs, det_samples.cpu(), B, ws, sd, R,
+                                     lambda r, idx: synth.frame_rows(B, idx, seed=100 + r))
 
     if rank == 0:
         line = {
@@ -310,6 +323,38 @@ def main():
         print(json.dumps(line), flush=True)
     if ws > 1:
         dist.destroy_process_group()
+
+
+def sample_local(B: int) -> list[int]:
+    """Frames of each rank's shard whose gathered records rank 0 checks at N > 1."""
+    return sorted({0, B // 2, B - 1})
+
+
+def gathered_parity(recs, det_samples, B, ws, sd, R, frames_of, stride=STRIDE):
+    """Config 5 parity: the all-gathered frame records (dets [G,300,6], cnt [G], emb [G,512],
+    norm [G,1], keypoints + scores [G,17,3], G = B*ws, rank order) on the sampled frames of
+    every rank's shard vs the oracle ``R`` on the same frames (``frames_of(r, idx)`` regenerates
+    rank r's inputs): keypoint OKS delta and embedding max|d| against the oracle forward, and
+    NMS rows exact against the oracle NMS of the rank's own det rows (``det_samples``
+    [ws*len(idx), 5, A], gathered in rank order)."""
+    import torch
+    dets, cnt, emb, _norm, kp = recs
+    idx = sample_local(B)
+    out = {"frames": [], "oks_delta": 0.0, "emb_max_abs": 0.0, "cls_max_abs": 0.0, "nms_exact": True,
+           "checked": "all-gathered records of sampled frames of every rank vs the oracle"}
+    with torch.no_grad():
+        for r in range(ws):
+            g = [r * B + i for i in idx]
+            ds = det_samples[r * len(idx):(r + 1) * len(idx)]
+            ref = R.forward_all(sd, frames_of(r, idx), stride=stride)
+            rc, _ = R.keypoints_from_heatmaps(ref["heatmaps"])
+            out["oks_delta"] = max(out["oks_delta"], R.oks_delta(kp[g][..., :2], rc))
+            out["emb_max_abs"] = max(out["emb_max_abs"], float((emb[g] - ref["emb"]).abs().max()))
+            out["cls_max_abs"] = max(out["cls_max_abs"], float((ds[:, 4] - ref["det"][:, 4]).abs().max()))
+            for j, m in enumerate(R.non_max_suppression(ds)):
+                out["nms_exact"] &= int(cnt[g[j]]) == len(m) and bool(torch.equal(dets[g[j], :len(m)], m))
+            out["frames"] += g
+    return out
 
 
 def cpu_legs(cfg, sd, x, o, B, reps):

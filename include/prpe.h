@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PRPE_ABI_VERSION 4
+#define PRPE_ABI_VERSION 5
 
 /* activations (epilogues/prologues) */
 enum prpe_act {
@@ -136,8 +136,17 @@ typedef struct prpe_conv_desc {
   const float* bias2;
   int32_t act2;
   int32_t n2;
+  /* caller-owned device scratch, >= prpe_conv2d_workspace_bytes(d) bytes, 256-B aligned (NULL and
+   * 0 when that is 0). Only the split-K path of full-window linears uses it (the IR-50 output
+   * layer: partial sums per K-slice); a call that needs more than it is given returns -EINVAL.
+   * Concurrent calls on different streams must pass different workspaces. */
+  void* workspace;
+  int64_t workspace_bytes;
 } prpe_conv_desc;
 
+/* Scratch bytes prpe_conv2d(d) needs (0 for every path but split-K), or -EINVAL for a descriptor
+ * prpe_conv2d would reject. Host-only: no launch, no allocation. */
+int64_t prpe_conv2d_workspace_bytes(const prpe_conv_desc* d);
 int prpe_conv2d(const prpe_conv_desc* d, void* stream);
 
 /*
@@ -314,9 +323,12 @@ int prpe_det_eval_loss(const float* boxes, const int64_t* box_strides, const flo
                        const int64_t* gt_batch, const int64_t* gt_classes, int32_t G, float* per_image,
                        float* loss, void* stream);
 
-/* ABI version / build info. */
+/* ABI version / build info. prpe_source_hash: sha256 (hex) of the sources the library was built
+ * from (csrc/*.hip, csrc/*.h, include/prpe.h; computed by build.py), so a host binding can refuse
+ * a library built from other sources than the ones beside it. */
 int prpe_abi_version(void);
 const char* prpe_build_info(void);
+const char* prpe_source_hash(void);
 
 #ifdef __cplusplus
 }

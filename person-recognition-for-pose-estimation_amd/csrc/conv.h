@@ -134,6 +134,7 @@ bool conv_gemm_eligible(const ConvK& kp, int prec);
 int conv_gemm_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 bool conv_splitk_eligible(const ConvK& kp, int prec, int k_order);
-int conv_splitk_launch(const ConvK& kp, hipStream_t st);
+int64_t conv_splitk_workspace_bytes(const ConvK& kp);
+int conv_splitk_launch(const ConvK& kp, float* workspace, hipStream_t st);
 
 }  // namespace prpe_k

@@ -559,7 +559,10 @@ int launch_cfg(const ConvK& kp0, int km, int prec, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
+// Validate a descriptor and fill the kernel arguments (shared by prpe_conv2d and
+// prpe_conv2d_workspace_bytes). Returns 0 or PRPE_EINVAL; km = the K walk (0 scalar, 1 vector,
+// 2 chunk-major).
+static int conv_setup(const prpe_conv_desc* d, ConvK& kp, int& km) {
   if (!d || !view_ok(&d->x) || !view_ok(&d->y) || !d->w_hi) return PRPE_EINVAL;
   if (d->precision < 0 || d->precision > 3) return PRPE_EINVAL;
   if ((d->precision == 0 || d->precision == 2) && !d->w_lo) return PRPE_EINVAL;
@@ -595,14 +598,14 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
                    (x.sn % 4) == 0 && ((uintptr_t)x.ptr % 16) == 0;
   // chunk-major K needs the vector path and whole 32-channel chunks
   if (d->k_order == 1 && (!vec || x.c % 32 != 0)) return PRPE_EINVAL;
-  const int km = d->k_order == 1 ? 2 : (vec ? 1 : 0);
+  km = d->k_order == 1 ? 2 : (vec ? 1 : 0);
   if (km == 0 && d->k_pad > 1024) return PRPE_EINVAL;
   // the input-side affine is implemented on the vector paths only (IR-50 pre-BN, Ci >= 64);
   // the vector paths keep one validity bit per kh and per kw
   if (km == 0 && d->in_scale) return PRPE_EINVAL;
   if (km != 0 && (d->kh > 32 || d->kw > 32)) return PRPE_EINVAL;
 
-  ConvK kp{};
+  kp = ConvK{};
   kp.x = x.ptr; kp.xsn = x.sn; kp.xsh = x.sh; kp.xsw = x.sw; kp.xsc = x.sc;
   kp.Hi = x.h; kp.Wi = x.w; kp.Ci = x.c;
   kp.y = y.ptr; kp.ysn = y.sn; kp.ysh = y.sh; kp.ysw = y.sw; kp.ysc = y.sc;
@@ -654,30 +657,59 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   kp.ylin = y.sh == (int64_t)Wo * y.sw && y.sn == (int64_t)Ho * y.sh;
   kp.rlin = d->res_mode == PRPE_RES_NONE ||
             (d->res.sh == (int64_t)Wo * d->res.sw && d->res.sn == (int64_t)Ho * d->res.sh);
-  {
-    // per-device address of the zero page (one host query per device, then cached)
-    static const float* zero_by_dev[64] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return PRPE_EINVAL;
-    if (!zero_by_dev[dev]) {
-      void* zp = nullptr;
-      if (hipGetSymbolAddress(&zp, HIP_SYMBOL(g_zero8)) != hipSuccess || !zp) return PRPE_EINVAL;
-      zero_by_dev[dev] = static_cast<const float*>(zp);
-    }
-    kp.zero = zero_by_dev[dev];
+  return 0;
+}
+
+// per-device address of the zero page (one host query per device, then cached)
+static const float* zero_page() {
+  static const float* zero_by_dev[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!zero_by_dev[dev]) {
+    void* zp = nullptr;
+    if (hipGetSymbolAddress(&zp, HIP_SYMBOL(g_zero8)) != hipSuccess || !zp) return nullptr;
+    zero_by_dev[dev] = static_cast<const float*>(zp);
   }
+  return zero_by_dev[dev];
+}
+
+// full-window linears with few M x N tiles (the IR-50 output layer): split along K
+// (conv_splitk.hip) automatically; tile 50 forces it
+static bool conv_use_splitk(const prpe_conv_desc* d, const ConvK& kp) {
+  if (d->tile == 50) return true;
+  return d->tile == 0 && kp.K >= 4096 && (int64_t)((kp.M + 63) / 64) * (kp.Co / 64) < 256 &&
+         conv_splitk_eligible(kp, d->precision, d->k_order);
+}
+
+extern "C" int64_t prpe_conv2d_workspace_bytes(const prpe_conv_desc* d) {
+  ConvK kp;
+  int km = 0;
+  if (conv_setup(d, kp, km) != 0) return PRPE_EINVAL;
+  if (!conv_use_splitk(d, kp) || !conv_splitk_eligible(kp, d->precision, d->k_order)) return 0;
+  return conv_splitk_workspace_bytes(kp);
+}
+
+extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
+  ConvK kp;
+  int km = 0;
+  if (int rc = conv_setup(d, kp, km)) return rc;
+  kp.zero = zero_page();
+  if (!kp.zero) return PRPE_EINVAL;
+  const prpe_view& x = d->x; const prpe_view& y = d->y;
+  const bool dual = d->x2.ptr != nullptr;
   hipStream_t st = as_stream(stream);
   const int prec = d->precision;
   int tile = d->tile;
   // direct fp32 kernel for tiny Co (needs the 3 weight planes; exact fp32 products); 1x1 only:
   // for 3x3 Co=3 the MFMA path measured faster (7.5 ms vs 11.8 ms at bs=256)
   const int khw = d->kh * d->kw;
-  // full-window linears with few M x N tiles (the IR-50 output layer): split along K
-  // (conv_splitk.hip); tile 50 forces it
-  if (tile == 50) return conv_splitk_eligible(kp, prec, d->k_order) ? conv_splitk_launch(kp, st) : PRPE_EINVAL;
-  if (tile == 0 && kp.K >= 4096 && (int64_t)((kp.M + 63) / 64) * (kp.Co / 64) < 256 &&
-      conv_splitk_eligible(kp, prec, d->k_order))
-    return conv_splitk_launch(kp, st);
+  // split-K: partial sums in the caller's workspace (prpe_conv2d_workspace_bytes)
+  if (conv_use_splitk(d, kp)) {
+    if (!conv_splitk_eligible(kp, prec, d->k_order)) return PRPE_EINVAL;
+    const int64_t need = conv_splitk_workspace_bytes(kp);
+    if (!d->workspace || d->workspace_bytes < need || (uintptr_t)d->workspace % 256) return PRPE_EINVAL;
+    return conv_splitk_launch(kp, static_cast<float*>(d->workspace), st);
+  }
   // epilogue 1x1 GEMM: the haloed-tile kernel's 128-column tile is the only implementation
   if (kp.w2) return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile ? tile : 31, st) : PRPE_EINVAL;
   if (tile == 0 && y.c <= 4 && km == 1 && !d->in_scale && d->w_lo && d->w_lo2 && x.c <= 256 && khw == 1) {

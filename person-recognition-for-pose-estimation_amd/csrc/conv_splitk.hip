@@ -12,7 +12,8 @@
 // pair as at precision 0 everywhere. Raw partial sums -> workspace [S][M][Co].
 // Stage 2 (linear_splitk_reduce): y = EPI(sum_s part[s]) in slice order (deterministic), with
 // the epilogue's scale / bias / activation.
-// The workspace is a per-device buffer owned by the library (grown on first use).
+// The partial sums go to the caller's workspace (prpe_conv2d_workspace_bytes; the library
+// never allocates), so concurrent calls on different streams use different buffers.
 #include "conv.h"
 
 namespace prpe_k {
@@ -104,28 +105,26 @@ bool conv_splitk_eligible(const ConvK& kp, int prec, int k_order) {
          (!kp.slope || (uintptr_t)kp.slope % 16 == 0);
 }
 
-int conv_splitk_launch(const ConvK& kp, hipStream_t st) {
-  // one K-slice per tap when the taps are >= 256 deep, else slices of 8 K-steps
+// one K-slice per tap when the taps are >= 256 deep, else slices of 8 K-steps
+static int splitk_slice(const ConvK& kp) {
   int kslice = kp.KH * kp.KW > 1 && kp.Ci >= 256 ? kp.Ci : 256;
   if (kp.K % kslice) kslice = 32;
+  return kslice;
+}
+
+int64_t conv_splitk_workspace_bytes(const ConvK& kp) {
+  const int64_t S = kp.K / splitk_slice(kp);
+  return S * kp.M * kp.Co * (int64_t)sizeof(float);
+}
+
+int conv_splitk_launch(const ConvK& kp, float* ws, hipStream_t st) {
+  const int kslice = splitk_slice(kp);
   const int S = kp.K / kslice;
-  const size_t need = (size_t)S * kp.M * kp.Co * sizeof(float);
-  static float* ws[64] = {};
-  static size_t wsz[64] = {};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return PRPE_EINVAL;
-  if (wsz[dev] < need) {
-    if (ws[dev]) (void)hipFree(ws[dev]);
-    ws[dev] = nullptr;
-    wsz[dev] = 0;
-    if (hipMalloc(&ws[dev], need) != hipSuccess) return PRPE_EINVAL;
-    wsz[dev] = need;
-  }
   const dim3 g1(kp.Co / 64, (kp.M + 63) / 64, S);
-  hipLaunchKernelGGL(linear_splitk_kernel, g1, dim3(256), 0, st, kp, ws[dev], kslice);
+  hipLaunchKernelGGL(linear_splitk_kernel, g1, dim3(256), 0, st, kp, ws, kslice);
   const int64_t total4 = (int64_t)kp.M * kp.Co / 4;
   hipLaunchKernelGGL(linear_splitk_reduce, dim3((unsigned)((total4 + 255) / 256)), dim3(256), 0, st, kp,
-                     (const float*)ws[dev], S);
+                     (const float*)ws, S);
   return launch_status();
 }
 

@@ -49,11 +49,8 @@ constexpr int BK = 32;
 // output's pixel grid, e.g. a stride-2 subsampling of the block input).
 // APL: the input tensor is stored as interleaved bf16 planes (see prpe.h, "planes format"):
 // the 32 bytes a lane loads for 8 channels already are the hi and lo fragments, no split.
-// ABL (diagnostic builds only, tiles 40..47 of tools/conv_bench.py; outputs are WRONG): bit 0 = no
-// B refresh in the loop (the prologue's stage is re-read), bit 1 = no A loads in the loop, bit 2
-// = no block barrier in the loop (vmcnt wait kept)
 template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false,
-          bool APL = false, int ABL = 0>
+          bool APL = false>
 __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   static_assert(!APL || (NP == 2 && !F16 && !PRO && !DUAL), "planes input: two bf16 planes only");
   static_assert(!F16 || (NP == 2 && !PRO), "f16 planes: two planes, no prologue");
@@ -259,10 +256,9 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   int st = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // B(kt) of this wave: at most the (STAGES-2)*IB pieces issued after it are still pending
-    if constexpr (ABL & 4) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((STAGES - 2) * IB) : "memory");
-    else wait_barrier<(STAGES - 2) * IB>();
-    if constexpr (!(ABL & 2)) load_a();
-    if constexpr (!(ABL & 1)) {
+    wait_barrier<(STAGES - 2) * IB>();
+    load_a();
+    {
       const int ks = kt + STAGES - 1 < nk ? kt + STAGES - 1 : nk - 1;
       const int sn = st == 0 ? STAGES - 1 : st - 1;   // the stage read at kt-1
       issue_b(ks, sn);
@@ -383,7 +379,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   }
 }
 
-template <int NW, int TM, int TN, int NP, int STAGES, bool F16 = false, int ABL = 0>
+template <int NW, int TM, int TN, int NP, int STAGES, bool F16 = false>
 int launch(const ConvK& kp0, hipStream_t st) {
   constexpr int BM = NW * TM * 16, BN = TN * 16;
   ConvK kp = kp0;
@@ -399,11 +395,10 @@ int launch(const ConvK& kp0, hipStream_t st) {
   }
   if (kp.x_planes) {
     if constexpr (F16 || NP != 2) return PRPE_EINVAL;
-    else hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, false, false, true, ABL>), dim3(kp.nwg),
+    else hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, false, false, true>), dim3(kp.nwg),
                             dim3(NW * 64), 0, st, kp);
     return launch_status();
   }
-  if constexpr (ABL != 0) return PRPE_EINVAL;
   if constexpr (F16)
     hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
   else if (kp.in_scale)
@@ -477,12 +472,6 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       case 27: return launch<2, 4, 8, 2, 3>(kp, st);   // 128 x 128, wave 64 x 128, 2 waves
       case 28: return launch<4, 2, 8, 2, 2>(kp, st);   // 128 x 128, wave 32 x 128, 2 stages
       case 29: return launch<4, 4, 8, 2, 2>(kp, st);   // 256 x 128, wave 64 x 128, 2 stages
-      // diagnostic ablations of tile 28 (planes input only; outputs wrong): see ABL
-      case 41: return launch<4, 2, 8, 2, 2, false, 1>(kp, st);
-      case 42: return launch<4, 2, 8, 2, 2, false, 2>(kp, st);
-      case 43: return launch<4, 2, 8, 2, 2, false, 3>(kp, st);
-      case 44: return launch<4, 2, 8, 2, 2, false, 4>(kp, st);
-      case 47: return launch<4, 2, 8, 2, 2, false, 7>(kp, st);
       default: return PRPE_EINVAL;
     }
   }

@@ -376,4 +376,4 @@ extern "C" int prpe_softargmax(const float* heat, int32_t B, int32_t K, int32_t 
 }
 
 extern "C" int prpe_abi_version(void) { return PRPE_ABI_VERSION; }
-extern "C" const char* prpe_build_info(void) { return "prpe gfx950 (CDNA4) split-bf16x3 MFMA; " __DATE__; }
+// prpe_build_info / prpe_source_hash: generated by build.py (build/build_info.c)

@@ -1,17 +1,20 @@
 """ctypes binding of libprpe.so (the C ABI declared in include/prpe.h).
 
 This is the only way the product reaches the device kernels: there is no CPU or
-PyTorch fallback. ``lib()`` raises if the library is missing or stale, and every call
-raises ``PrpeError`` on a non-zero status.
+PyTorch fallback. ``lib()`` raises if the library is missing, was built for another ABI
+version, or was built from other sources than the ones beside it (``prpe_source_hash``
+against prpe/_srchash.py), and every call raises ``PrpeError`` on a non-zero status.
 """
 from __future__ import annotations
 
 import ctypes as C
 import os
 
+from ._srchash import source_hash
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libprpe.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class PrpeError(RuntimeError):
@@ -38,7 +41,7 @@ class ConvDesc(C.Structure):
                 ("x2", View), ("x2_amax", C.c_void_p), ("x_planes", C.c_int32), ("y_planes", C.c_int32),
                 ("w2", C.c_void_p), ("y2", View),
                 ("w3", C.c_void_p), ("scale2", C.c_void_p), ("bias2", C.c_void_p), ("act2", C.c_int32),
-                ("n2", C.c_int32)]
+                ("n2", C.c_int32), ("workspace", C.c_void_p), ("workspace_bytes", C.c_int64)]
 
 
 ACT = {"none": 0, "relu": 1, "silu": 2, "prelu": 3, "gelu": 4, "sigmoid": 5}
@@ -51,6 +54,7 @@ _L = C.c_int64
 _F = C.c_float
 _VP = C.POINTER(View)
 SIGNATURES = {
+    "prpe_conv2d_workspace_bytes": (C.c_int64, [C.POINTER(ConvDesc)]),
     "prpe_conv2d": (C.c_int, [C.POINTER(ConvDesc), _P]),
     "prpe_upconv3x3_workspace_bytes": (C.c_int64, [_VP, _VP]),
     "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _I, _P, _L, _P]),
@@ -77,6 +81,7 @@ SIGNATURES = {
     "prpe_det_eval_loss": (C.c_int, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _I, _P, _P, _P]),
     "prpe_abi_version": (C.c_int, []),
     "prpe_build_info": (C.c_char_p, []),
+    "prpe_source_hash": (C.c_char_p, []),
 }
 
 _lib = None
@@ -97,8 +102,20 @@ def lib():
             f.argtypes = args
         if L.prpe_abi_version() != ABI_VERSION:
             raise PrpeError("libprpe.so ABI version mismatch; rebuild")
+        check_source_hash(L.prpe_source_hash().decode())
         _lib = L
     return _lib
+
+
+def check_source_hash(built: str, present: str | None = None):
+    """Refuse a library built from other sources than the ones beside it (a stale prebuilt
+    .so would otherwise load silently). ``present`` defaults to the hash of the sources on disk."""
+    present = source_hash() if present is None else present
+    if present is None:
+        raise PrpeError("prpe sources (csrc/, include/prpe.h) not found beside libprpe.so: cannot verify the build")
+    if built != present:
+        raise PrpeError(f"{LIB_PATH} is stale: built from sources {built[:16]}, the sources here hash to "
+                        f"{present[:16]}; rebuild with `python person-recognition-for-pose-estimation_amd/build.py`")
 
 
 def check(status: int, what: str):

@@ -11,6 +11,8 @@ collective and trimmed afterwards.
 """
 from __future__ import annotations
 
+import math
+
 import torch
 import torch.distributed as dist
 
@@ -70,7 +72,8 @@ def gather_frame_records(parts, global_batch: int | None = None, group=None):
     for t in parts:
         if t.shape[0] != b or t.dtype not in (torch.float32, torch.int32):
             raise ValueError("gather_frame_records: [b, ...] float32 / int32 tensors of one batch")
-        flat.append(t.contiguous().view(torch.float32).reshape(b, -1))
+        # explicit per-frame width: an empty shard (global batch < world) has b = 0
+        flat.append(t.contiguous().view(torch.float32).reshape(b, math.prod(t.shape[1:])))
     rec = gather_tensor(torch.cat(flat, 1), global_batch, group)
     out, o = [], 0
     for t, f in zip(parts, flat):

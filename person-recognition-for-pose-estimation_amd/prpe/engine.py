@@ -38,7 +38,7 @@ BN_EPS = 1e-5
 # multiplies logit errors by the stride; the large adapters and the ViT run the bf16 3-term
 # split.
 AUTO_POLICY = {"trunk": 3, "yolo_adapter": 0, "yolo_net": 2, "adaface": 0, "vit": 0}
-AMAX_TENSORS = 128                  # max|y| slot arrays per forward (one [B] array per conv output)
+AMAX_CHUNK = 1 << 16                # floats per chunk of a component's max|y| slot pool
 # PRPE_PLANES=0 keeps every activation in fp32 (A/B runs of the planes-format handoff)
 PLANES_ON = os.environ.get("PRPE_PLANES", "1") != "0"
 # 3x3/1 convs with Co <= 4 (the last conv of the YOLO and ViTPose adapters) as the tap rewrite
@@ -52,15 +52,21 @@ TAPS_FUSE = os.environ.get("PRPE_TAPS_FUSE", "1") != "0"
 
 
 class _Prec:
+    """Component scope: its precision from the policy and, at precision 3, its own max|y| slot
+    pool (zeroed on entry, on the current stream)."""
+
     def __init__(self, eng, comp):
         self.e, self.c = eng, comp
 
     def __enter__(self):
-        self.saved = self.e.precision
-        self.e.precision = self.e.policy.get(self.c, self.saved)
+        self.saved = (self.e.precision, self.e._amax_scope)
+        self.e.precision = self.e.policy.get(self.c, self.saved[0])
+        if self.e.precision == 3:
+            self.e._amax_begin(self.c)
 
     def __exit__(self, *a):
-        self.e.precision = self.saved
+        self.e.precision, scope = self.saved
+        self.e._amax_scope = scope
 
 
 class Engine:
@@ -80,9 +86,10 @@ class Engine:
         self._aux: dict[str, torch.Tensor] = {}
         self.watch: set[str] = set()      # pack names whose launches get HIP-event timing
         self.events: dict[str, list] = {}
-        self._amax_pool = None             # device per-frame max|y| slots of conv outputs (precision 3)
-        self._amax_i = 0
-        self._amax_b = 1
+        # per-component device pools of per-frame max|y| slots (precision 3): comp -> [chunk
+        # tensors, cursor (chunk index, offset)]
+        self._amax_pools: dict[str, list] = {}
+        self._amax_scope = None
 
     def prec(self, comp):
         return _Prec(self, comp)
@@ -118,24 +125,34 @@ class Engine:
             self._packs[name] = p
         return p
 
-    # ---- max|y| tracking: every precision-3 conv output gets a [B] array of per-FRAME device
-    # slots its epilogue raises to max|y[n]|; a precision-3 consumer reads slot n to pick frame
-    # n's activation scale, so a frame's arithmetic never depends on its batch-mates (or on the
-    # shard it lands in). The pool is zeroed once per forward (amax_reset, start of the trunk).
-    def amax_reset(self, batch: int):
-        n = AMAX_TENSORS * batch
-        if self._amax_pool is None or self._amax_pool.numel() < n:
-            self._amax_pool = torch.zeros(n, device=self.device, dtype=torch.float32)
-        else:
-            self._amax_pool.zero_()
-        self._amax_i = 0
-        self._amax_b = batch
+    # ---- max|y| tracking: every conv output of a precision-3 component gets an [N] array of
+    # per-row-group device slots (N = the conv's leading dim: frames, or tokens for the ViT's
+    # [B*L, 1, 1, D] linears) its epilogue raises to max|y[n]|; a precision-3 consumer reads slot
+    # n to pick row group n's activation scale, so a frame's arithmetic never depends on its
+    # batch-mates (or on the shard it lands in). Each component scope (Engine.prec) owns a pool
+    # of chunks, zeroed on entry on the current stream (the heads run on their own streams) and
+    # grown by whole chunks on first use, so any batch and any number of convs fit.
+    def _amax_begin(self, comp: str):
+        pool = self._amax_pools.get(comp)
+        if pool is None:
+            pool = self._amax_pools[comp] = [[], 0, 0]
+        for t in pool[0]:
+            t.zero_()
+        pool[1] = pool[2] = 0
+        self._amax_scope = comp
 
-    def amax_slot(self, batch: int):
-        if self._amax_pool is None or batch != self._amax_b or self._amax_i >= AMAX_TENSORS:
-            raise RuntimeError("max|y| slot pool not reset for this batch (Engine.amax_reset)")
-        t = self._amax_pool[self._amax_i * batch:(self._amax_i + 1) * batch]
-        self._amax_i += 1
+    def amax_slot(self, n: int):
+        """[n] zeroed slots from the current precision-3 component's pool."""
+        if self._amax_scope is None:
+            raise RuntimeError("max|y| slots requested outside a precision-3 component scope (Engine.prec)")
+        pool = self._amax_pools[self._amax_scope]
+        chunks, ci, off = pool
+        if ci < len(chunks) and off + n > chunks[ci].numel():
+            ci, off = ci + 1, 0
+        if ci == len(chunks):
+            chunks.append(torch.zeros(max(AMAX_CHUNK, n), device=self.device, dtype=torch.float32))
+        t = chunks[ci][off:off + n]
+        pool[1], pool[2] = ci, off + n
         return t
 
     @staticmethod
@@ -244,7 +261,6 @@ class Engine:
     def trunk(self, x_nchw, flip_w=False):
         """MultiTaskResNetFeatureExtractor (modify_models.py:427-437), torchvision v1.5.
         ``flip_w``: run on the W-mirrored frames (torch.flip(images, dims=[-1]))."""
-        self.amax_reset(x_nchw.shape[0])
         with self.prec("trunk"):
             return self._trunk(x_nchw, flip_w)
 

@@ -10,7 +10,7 @@ import ctypes as C
 
 import torch
 
-from ._lib import ACT, RES_NONE, ConvDesc, View, check, lib
+from ._lib import ACT, RES_NONE, ConvDesc, PrpeError, View, check, lib
 
 
 def _stream() -> C.c_void_p:
@@ -95,6 +95,15 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
     d.precision = precision
     d.tile = tile
     d.k_order = pack.k_order
+    # caller-owned scratch (the split-K partial sums; 0 bytes on every other path), from the
+    # caching allocator on the current stream, so concurrent streams never share one
+    nbytes = lib().prpe_conv2d_workspace_bytes(C.byref(d))
+    if nbytes < 0:
+        raise PrpeError(f"prpe_conv2d[{pack.name}]: descriptor rejected (status {nbytes})")
+    ws = None
+    if nbytes:
+        ws = torch.empty((nbytes + 255) // 256 * 64, device=y.device, dtype=torch.float32)
+        d.workspace, d.workspace_bytes = ws.data_ptr(), nbytes
     check(lib().prpe_conv2d(C.byref(d), _stream()), f"prpe_conv2d[{pack.name}]")
     return y
 

@@ -63,6 +63,22 @@ def frames(batch: int, height: int = 640, width: int = 640, seed: int = INPUT_SE
     return uniform(seed, f"{name}:{batch}x{height}x{width}", (batch, 3, height, width))
 
 
+def frame_rows(batch: int, rows, height: int = 640, width: int = 640, seed: int = INPUT_SEED,
+               name: str = "frames") -> torch.Tensor:
+    """``frames(batch, ...)[rows]`` bit for bit, generating only those frames (the stream is
+    counter-based: frame f is elements f*3*H*W .. (f+1)*3*H*W of the same stream)."""
+    per = 3 * height * width
+    base = np.uint64(_key_hash(seed, f"{name}:{batch}x{height}x{width}"))
+    out = np.empty((len(rows), per), dtype=np.float32)
+    for j, f in enumerate(rows):
+        if not 0 <= f < batch:
+            raise IndexError(f"frame {f} outside a batch of {batch}")
+        with np.errstate(over="ignore"):
+            ctr = base + np.arange(f * per, (f + 1) * per, dtype=np.uint64)
+        out[j] = (splitmix64(ctr) >> np.uint64(40)).astype(np.float32) * np.float32(2.0 ** -24)
+    return torch.from_numpy(out.reshape(len(rows), 3, height, width))
+
+
 def _is_residual_branch_tail(name: str) -> bool:
     return (name.endswith("bn3.weight")                                   # ResNet bottleneck
             or name.endswith("res_layer.5.weight")                        # IR-50 BasicBlockIR

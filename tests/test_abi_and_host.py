@@ -53,6 +53,50 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert L.prpe_conv2d(C.byref(d), None) == -22
 
 
+def test_library_refuses_other_sources(monkeypatch):
+    """lib() compares the source hash compiled into libprpe.so (build.py) with the hash of the
+    sources beside it and refuses a library built from other sources."""
+    from prpe import _srchash
+    L = _lib.lib()
+    built = L.prpe_source_hash().decode()
+    assert len(built) == 64 and built == _srchash.source_hash()
+    assert built[:16].encode() in L.prpe_build_info()
+    _lib.check_source_hash(built)                                          # fresh: accepted
+    with pytest.raises(_lib.PrpeError, match="stale"):
+        _lib.check_source_hash(built, present="0" * 64)
+    # the whole load path: sources that hash differently -> lib() raises
+    monkeypatch.setattr(_lib, "_lib", None)
+    monkeypatch.setattr(_lib, "source_hash", lambda: "f" * 64)
+    with pytest.raises(_lib.PrpeError, match="stale"):
+        _lib.lib()
+
+
+def test_conv_workspace_is_caller_owned():
+    """Split-K (IR-50 output layer geometry, M = 256 frames, K = 7*7*512, Co = 512): the
+    library reports the partial-sum bytes it needs and never allocates them; every other
+    path needs none. Host-only queries (no GPU here)."""
+    L = _lib.lib()
+    x = _lib.View(0x10000, 256, 7, 7, 512, 7 * 7 * 512, 7 * 512, 512, 1)
+    y = _lib.View(0x20000, 256, 1, 1, 512, 512, 512, 512, 1)
+    d = _lib.ConvDesc(x=x, y=y, kh=7, kw=7, stride=1, pad=0, w_hi=0x1000, w_lo=0x1000, w_lo2=0x1000,
+                      k_pad=25088, co_pad=512, precision=0, k_order=0)
+    assert L.prpe_conv2d_workspace_bytes(C.byref(d)) == 49 * 256 * 512 * 4     # one K-slice per tap
+    d.tile = 4                                                                # a non-split tile
+    assert L.prpe_conv2d_workspace_bytes(C.byref(d)) == 0
+    d.tile = 0
+    d.k_pad = 100                                                             # invalid pack
+    assert L.prpe_conv2d_workspace_bytes(C.byref(d)) == -22
+    v = _lib.View(0x1000, 1, 4, 4, 32, 512, 128, 32, 1)
+    d = _lib.ConvDesc(x=v, y=v, kh=1, kw=1, stride=1, pad=0, w_hi=0x1000, w_lo=0x1000, w_lo2=0x1000,
+                      k_pad=32, co_pad=128, precision=0)
+    assert L.prpe_conv2d_workspace_bytes(C.byref(d)) == 0
+    src = open(os.path.join(ROOT, "person-recognition-for-pose-estimation_amd", "csrc", "conv_splitk.hip")).read()
+    import glob
+    for f in glob.glob(os.path.join(ROOT, "person-recognition-for-pose-estimation_amd", "csrc", "*")):
+        assert not re.search(r"\bhip(Malloc|Free)\w*\s*\(", open(f).read()), f"{f} allocates device memory"
+    assert "workspace" in src
+
+
 def test_state_dict_spec_is_complete():
     spec = arch.state_dict_spec()
     assert len(spec) == 2130

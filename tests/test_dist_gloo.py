@@ -49,7 +49,7 @@ def _check(out, world, gb):
         assert kp.shape == (gb, 17, 3) and torch.equal(kp, fr[:, None, None].float() * 0.5 + torch.zeros(gb, 17, 3))
 
 
-@pytest.mark.parametrize("world,gb", [(2, 6), (4, 7)])
+@pytest.mark.parametrize("world,gb", [(2, 6), (4, 7), (4, 3)])
 def test_gather_detections_gloo(tmp_path, world, gb):
     port = _free_port()
     out = str(tmp_path / "res")
@@ -78,3 +78,28 @@ def test_bench_launcher_spawns_ranks(tmp_path, monkeypatch):
         assert torch.load(f"{out}.{r}", weights_only=True)["local_rank"] == r
     # a failing rank makes the launcher fail
     assert bench.launch_children(2, [sys.executable, "-c", "import os,sys; sys.exit(int(os.environ['RANK']) + 3)"]) != 0
+
+
+def test_gathered_parity_gloo(tmp_path):
+    """Config 5's rank-0 check (bench.gathered_parity) over gloo, world size 2: CPU stand-in
+    ranks make their shard's records with the oracle, the records travel through the same
+    all-gathers as in bench.py, rank 0 finds them exact; two frames' records swapped in
+    transit are caught (OKS / embedding / NMS mismatch)."""
+    port = _free_port()
+    out = str(tmp_path / "parity")
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="2", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_dist_parity_worker.py"), out, "2", "64"],
+                                      env=env))
+    for p in procs:
+        assert p.wait(timeout=300) == 0
+    res = torch.load(out, weights_only=True)
+    good, bad = res["good"], res["bad"]
+    assert good["frames"] == [0, 1, 2, 3]
+    # same oracle, same frames: equal up to CPU batch-composition rounding (OKS of equal
+    # coordinates is 1 - 3e-13 in its float64 arithmetic)
+    assert good["oks_delta"] < 1e-9 and good["emb_max_abs"] < 1e-5 and good["cls_max_abs"] < 1e-5
+    assert good["nms_exact"] is True
+    assert bad["emb_max_abs"] > 1e-3 and bad["nms_exact"] is False and bad["oks_delta"] > 1e-6

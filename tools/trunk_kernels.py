@@ -26,19 +26,18 @@ def main():
     e = CombinedModel(sd, precision="auto").engine
     B = a.batch
     x = synth.frames(B).cuda()
-    with e.prec("trunk"):
-        if a.what == "stem":
-            for _ in range(a.iters):
-                e.amax_reset(B)
+    if a.what == "stem":
+        for _ in range(a.iters):
+            with e.prec("trunk"):              # each entry zeroes the trunk's max|y| slots
                 e.stem(x)
-        else:
-            e.amax_reset(B)
+    else:
+        with e.prec("trunk"):
             o = torch.relu(torch.randn(B, 160, 160, 64, device="cuda"))
             xs = torch.relu(torch.randn(B, 160, 160, 64, device="cuda"))
-            o._prpe_amax = o.abs().flatten(1).amax(1).contiguous()
-            xs._prpe_amax = xs.abs().flatten(1).amax(1).contiguous()
-            for _ in range(a.iters):
-                e.amax_reset(B)
+        o._prpe_amax = o.abs().flatten(1).amax(1).contiguous()
+        xs._prpe_amax = xs.abs().flatten(1).amax(1).contiguous()
+        for _ in range(a.iters):
+            with e.prec("trunk"):
                 e.conv(o, e.pk_dual("backbone.layer1.0"), x2=xs, x2_amax=xs._prpe_amax)
     torch.cuda.synchronize()
     print("ok", a.what, B)
