@@ -1,6 +1,6 @@
 """Benchmark: whole-node frames/s of the per-frame multi-task hot path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config full|yolo_face|vitpose] [--batch B]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config full|yolo_face|yolo_raw|vitpose] [--batch B]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N ...
 
@@ -11,6 +11,8 @@ Configs (BASELINE.json ``configs``; the bench line is config 4 by default):
              soft-argmax; for N > 1 the per-rank frame records (padded detections, embeddings,
              keypoints) are all-gathered over RCCL (the only exchange).
   yolo_face  config 2: 64 frames per GPU, trunk -> face-YOLO -> NMS.
+  yolo_raw   config 2's kernel micro-bench variant: YOLO v11n nc=1 straight on
+             64 raw 640x640 frames per GPU (A = 8400) -> NMS.
   vitpose    config 3: 256 pixel_values crops [3,256,192] per GPU -> ViTPose-B -> soft-argmax.
 Frames shard across ranks (each rank owns a contiguous slice of the global batch), weights are
 replicated, no collective on the data path; value = all ranks' frames / max-over-ranks time
@@ -27,7 +29,7 @@ Rank 0 prints ONE JSON line. Extra objects:
                  its in-region, co-resident time is reported beside it); achieved = its
                  algorithmic FLOPs per launch / mean launch time; peak = dense bf16 MFMA 2.5 PF/s.
                  ``traffic`` (HBM bytes per launch, PMC FETCH_SIZE x2 + WRITE_SIZE) comes from the
-                 committed profiles/r02_pmc_traffic_<config>.json only while the sources of that
+                 newest committed profiles/rNN_pmc_traffic_<config>.json only while the sources of that
                  kernel (the files listed there) hash to the value recorded there (else null,
                  "stale").
   cpu_baseline — the oracle (fp32 PyTorch-CPU restatement of the reference, pinned against the
@@ -64,6 +66,8 @@ CONFIGS = {
     "full": (256, ["vit_pose.adapter.7"], 4,
              "full multi-task model (trunk + face-YOLO + AdaFace + ViTPose + NMS + soft-argmax), 640x640"),
     "yolo_face": (64, ["yolo_face.adapter.10"], 2, "YOLO-face detection head (trunk + face-YOLO + NMS), 640x640"),
+    "yolo_raw": (64, ["yolo_face.yolo.net.p1.0"], 2,
+                 "YOLO v11n nc=1 on raw 640x640 frames (config-2 micro-bench variant, A=8400) + NMS"),
     "vitpose": (256, [f"vit_pose.vit_pose.backbone.encoder.layer.{i}:fc1" for i in range(12)], 3,
                 "ViTPose-B keypoint head on 256x192 crops (pixel_values -> heatmaps -> soft-argmax)"),
 }
@@ -204,6 +208,12 @@ def main():
                 # embedding + norm, keypoints + scores (prpe/dist.py)
                 o["gathered"] = gather_frame_records([dets, cnt, o["emb"], o["norm"],
                                                       torch.cat([coords, scores[..., None]], -1)])
+        elif cfg == "yolo_raw":
+            det = eng.yolo_raw("yolo_face", x, STRIDE)
+            dets, cnt = non_max_suppression_padded(det)
+            o = {"det": det, "dets": dets, "cnt": cnt}
+            if ws > 1:
+                gather_detections(dets, cnt)
         elif cfg == "yolo_face":
             det = eng.yolo("yolo_face", eng.trunk(x), STRIDE)
             dets, cnt = non_max_suppression_padded(det)
@@ -260,25 +270,33 @@ def main():
     roof = None
     if evs:
         ms = ev_ms(evs)
-        _, _, pixels, p, precn = evs[0]
+        _, _, pixels, p, precn, x_numel = evs[0]
         avg_s = sum(ms) / len(ms) / 1e3
         fl = conv_flops(p, pixels)
         passes = {0: 3, 1: 1, 2: 6, 3: 3}[precn]
-        ach = fl / avg_s / 1e12
         name = dominant[0] if len(dominant) == 1 else dominant[0].replace(".layer.0:", ".layer.*:")
-        roof = {"bound": "mfma", "kernel": f"prpe_conv2d[{name}] {p.kh}x{p.kw} {p.ci}->{p.co} "
-                                           f"(library's automatic kernel/tile choice, precision {precn})",
-                "achieved": round(ach, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
-                "executed_mfma_passes": passes,
-                "executed_frac": round(ach * passes / MFMA_BF16_PEAK_TFLOPS, 4),
-                "avg_launch_ms": round(sum(ms) / len(ms), 4), "launches": len(ms),
+        kern = (f"prpe_conv2d[{name}] {p.kh}x{p.kw}/{p.stride} {p.ci}->{p.co} "
+                f"(library's automatic kernel/tile choice, precision {precn})")
+        # algorithmic bytes: the input read once, the output written once, the fp32 weights once
+        nbytes = 4.0 * (x_numel + pixels * p.co + p.co * p.ci * p.kh * p.kw)
+        if fl / nbytes < MFMA_BF16_PEAK_TFLOPS / HBM_PEAK_GBS * 1e3:      # below the ridge: HBM-bound
+            ach = nbytes / avg_s / 1e9
+            roof = {"bound": "hbm", "kernel": kern, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_gb_per_launch": round(nbytes / 1e9, 4),
+                    "flop_per_byte": round(fl / nbytes, 2)}
+        else:
+            ach = fl / avg_s / 1e12
+            roof = {"bound": "mfma", "kernel": kern, "achieved": round(ach, 2), "peak": MFMA_BF16_PEAK_TFLOPS,
+                    "unit": "TFLOP/s", "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
+                    "executed_mfma_passes": passes, "executed_frac": round(ach * passes / MFMA_BF16_PEAK_TFLOPS, 4)}
+        roof.update({"avg_launch_ms": round(sum(ms) / len(ms), 4), "launches": len(ms),
                 "measured": ("isolated pass after the timed region (heads sequential)" if isolated
                              else "inside the timed region"),
                 "in_timed_region_ms": round(sum(timed) / len(timed), 4) if timed else None,
-                "algorithmic_gflop_per_launch": round(fl / 1e9, 2), "traffic": None}
-        tp = os.path.join(ROOT, "profiles", f"r02_pmc_traffic_{cfg}.json")
-        if os.path.exists(tp):
+                "algorithmic_gflop_per_launch": round(fl / 1e9, 2), "traffic": None})
+        recs = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_pmc_traffic_{cfg}.json")))
+        tp = recs[-1] if recs else ""                    # the newest round's record
+        if tp:
             t = json.load(open(tp))
             fresh = (t.get("sources_sha") == kernel_sources_hash(t.get("sources")) and t.get("batch") == B
                      and t.get("layer") in dominant and t.get("precision") == precn)
@@ -378,6 +396,9 @@ def cpu_legs(cfg, sd, x, o, B, reps):
         elif cfg == "yolo_face":
             det = R.yolo_branch(sd, "yolo_face", R.resnet50_trunk(sd, xs), STRIDE)
             parity["cls_max_abs"] = float((o["det"][idx, 4].cpu() - det[:, 4]).abs().max())
+        elif cfg == "yolo_raw":
+            det = R.yolo_net(sd, "yolo_face", xs, STRIDE)
+            parity["cls_max_abs"] = float((o["det"][idx, 4].cpu() - det[:, 4]).abs().max())
         else:
             heat = R.vitpose_backbone(sd, xs)
             parity["heatmaps_max_abs"] = float((o["heatmaps"][idx].cpu() - heat).abs().max())
@@ -399,6 +420,8 @@ def cpu_legs(cfg, sd, x, o, B, reps):
                 R.keypoints_from_heatmaps(r["heatmaps"])
             elif cfg == "yolo_face":
                 R.non_max_suppression(R.yolo_branch(sd, "yolo_face", R.resnet50_trunk(sd, xb), STRIDE))
+            elif cfg == "yolo_raw":
+                R.non_max_suppression(R.yolo_net(sd, "yolo_face", xb, STRIDE))
             else:
                 R.keypoints_from_heatmaps(R.vitpose_backbone(sd, xb))
 

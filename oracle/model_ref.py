@@ -154,6 +154,13 @@ def yolo_branch(sd, p, feat, stride=(0.0, 0.0, 0.0), calib=None):
     x = x - x.mean(dim=(2, 3), keepdim=True)                       # modify_models.py:84-86
     x = x / (x.std(dim=(2, 3), keepdim=True) + 1e-6)
     x = torch.sigmoid(x)
+    return yolo_net(sd, p, x, stride, calib)
+
+
+def yolo_net(sd, p, x, stride=(0.0, 0.0, 0.0), calib=None):
+    """yolopt ``YOLO.forward`` in eval mode (nn.py:294-297: net -> fpn -> head) on NCHW input:
+    the adapter's [B,3,160,160] (A = 525) or raw [B,3,640,640] frames (A = 8400, the config-2
+    micro-bench variant)."""
     n = p + ".yolo.net"
     x = _yc(sd, n + ".p1.0", x, 3, 2, calib=calib)
     x = _csp(sd, n + ".p2.1", _yc(sd, n + ".p2.0", x, 3, 2, calib=calib), False, calib)

@@ -206,7 +206,7 @@ class Engine:
             e0.record()
             ops.conv2d(x, p, out, **kw)
             e1.record()
-            self.events.setdefault(p.name, []).append((e0, e1, B * Ho * Wo, p, prec))
+            self.events.setdefault(p.name, []).append((e0, e1, B * Ho * Wo, p, prec, x.numel()))
         else:
             ops.conv2d(x, p, out, **kw)
         out._prpe_amax = ya
@@ -396,6 +396,13 @@ class Engine:
             s = self.yolo_adapter(p, feat)
         with self.prec("yolo_net"):
             return self.yolo_net(p, s, stride)
+
+    def yolo_raw(self, p, x_nchw, stride=(0.0, 0.0, 0.0)):
+        """yolopt ``YOLO.forward`` eval (nn.py:294-297) straight on frames [B,3,H,W] (NCHW,
+        read in place through an NHWC view): the config-2 micro-bench variant, A = 8400 at
+        640x640 -> [B, 5, A]."""
+        with self.prec("yolo_net"):
+            return self.yolo_net(p, ops.nhwc(x_nchw), stride)
 
     def yolo_adapter(self, p, feat):
         a = p + ".adapter"

@@ -144,6 +144,16 @@ class CombinedModel:
             return PoseOutput(heatmaps=e.vit_backbone(ops.nhwc(x)))
 
     @torch.no_grad()
+    def yolo_from_frames(self, branch, x):
+        """``model.<branch>.yolo(frames)``: yolopt ``YOLO.forward`` eval (nn.py:294-297) on
+        [B,3,H,W] frames (H, W multiples of 32) -> [B, 5, A] with the branch head's stride
+        (A = 8400 at 640x640; SURVEY.md §8d config-2 micro-bench variant)."""
+        x = self._check_input(x)
+        if x.shape[2] % 32 or x.shape[3] % 32:
+            raise ValueError("YOLO input H and W must be multiples of 32 (the P5 stride)")
+        return self.engine.yolo_raw(branch, x, self._stride(getattr(self, branch)))
+
+    @torch.no_grad()
     def forward_all(self, x, face_stride=None, concurrent=True):
         """Trunk once -> face-YOLO det, AdaFace (emb, norm), ViTPose heatmaps.
 

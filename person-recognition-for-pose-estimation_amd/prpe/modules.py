@@ -82,11 +82,30 @@ class VitPoseModule(ParamTree):
         return self._owner.vitpose_from_pixels(pixel_values)
 
 
+class YoloModule(ParamTree):
+    """``model.yolo_face.yolo`` / ``model.yolo_person.yolo``: the yolopt ``YOLO`` inside
+    ``CustomYOLO`` (modify_models.py:61-106). Calling it runs the HIP YOLO v11n (net -> fpn ->
+    head, eval) on frames [B,3,H,W] and returns [B, 4+nc, A] (nn.py:294-297; A = 8400 at
+    640x640: the config-2 micro-bench variant), with ``head.stride`` as set on this module."""
+
+    def __init__(self, owner, branch):
+        super().__init__()
+        object.__setattr__(self, "_owner", owner)
+        object.__setattr__(self, "_branch", branch)
+
+    def forward(self, x):
+        return self._owner.yolo_from_frames(self._branch, x)
+
+
 def branch_trees(sd: dict, owner) -> dict:
     """{'yolo_face', 'yolo_person', 'ada_face', 'vit_pose'} -> module trees (see module doc)."""
     out = {}
-    for name in ("yolo_face", "yolo_person", "ada_face"):
-        out[name] = build_tree(sd, name)
+    for name in ("yolo_face", "yolo_person"):
+        t = ParamTree()
+        build_tree(sd, name + ".adapter", t.child("adapter"))
+        t.add_module("yolo", build_tree(sd, name + ".yolo", YoloModule(owner, name)))
+        out[name] = t
+    out["ada_face"] = build_tree(sd, "ada_face")
     vit = ParamTree()
     build_tree(sd, "vit_pose.adapter", vit.child("adapter"))
     vit.add_module("vit_pose", build_tree(sd, "vit_pose.vit_pose", VitPoseModule(owner)))

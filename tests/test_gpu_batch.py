@@ -135,3 +135,43 @@ def test_config3_bs256_parity_on_spread_frames(model, state_dict):
     # frame independence on this path too
     h2 = model.vitpose_from_pixels(pix[[255, 0]].cuda()).heatmaps.cpu()
     assert torch.equal(h2[0], heat[255]) and torch.equal(h2[1], heat[0])
+
+
+def test_config2_micro_yolo_raw_frames_vs_reference_golden(model):
+    """Config-2 micro-bench variant: ``model.yolo_face.yolo(frames)`` -- YOLO
+    v11n nc=1 straight on raw 640x640 frames, A = 8400 -- against the reference's own output
+    (oracle/make_golden_yolo_raw.py), and the batched NMS at A = 8400 bit-exact against the
+    reference's yolopt NMS on the golden's tie-free det copy."""
+    with np.load(os.path.join(GOLDEN, "golden_yolo_raw.npz"), allow_pickle=False) as z:
+        g = {k: z[k] for k in z.files}
+    x = synth.frames(2).cuda()
+    model.yolo_face.yolo.head.stride = torch.tensor(STRIDE)
+    try:
+        det = model.yolo_face.yolo(x).cpu()
+    finally:
+        model.yolo_face.yolo.head.stride = torch.zeros(3)
+    ref = torch.from_numpy(g["det"])
+    assert det.shape == ref.shape == (2, 5, 8400)
+    assert (det[:, 4] - ref[:, 4]).abs().max().item() <= 1e-3
+    assert (det[:, :4] - ref[:, :4]).abs().max().item() <= 2e-3 * ref[:, :4].abs().max().item()
+    dets, cnt = non_max_suppression_padded(torch.from_numpy(g["det_tiefree"]).cuda())
+    assert cnt.cpu().tolist() == g["nms_count"].tolist()
+    for i, n in enumerate(g["nms_count"].tolist()):
+        assert torch.equal(dets[i, :n].cpu(), torch.from_numpy(g["nms_out"][i, :n]))
+    # the model's own (tied) scores: bit-exact against the oracle's stable-order NMS
+    dets, cnt = non_max_suppression_padded(det.cuda())
+    for i, m in enumerate(R.non_max_suppression(det)):
+        assert int(cnt[i]) == len(m) and torch.equal(dets[i, :len(m)].cpu(), m)
+
+
+def test_config2_micro_yolo_raw_bs64_parity(model, state_dict):
+    x = synth.frames(64, seed=4)
+    det = model.engine.yolo_raw("yolo_face", x.cuda(), STRIDE).cpu()
+    idx = spread(64)
+    with torch.no_grad():
+        ref = R.yolo_net(state_dict, "yolo_face", x[idx], STRIDE)
+    assert (det[idx, 4] - ref[:, 4]).abs().max().item() <= 1e-3
+    assert (det[idx, :4] - ref[:, :4]).abs().max().item() <= 2e-3 * ref[:, :4].abs().max().item()
+    # frame independence on this path
+    d2 = model.engine.yolo_raw("yolo_face", x[[63, 0]].cuda(), STRIDE).cpu()
+    assert torch.equal(d2[0], det[63]) and torch.equal(d2[1], det[0])

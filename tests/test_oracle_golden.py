@@ -93,3 +93,21 @@ def test_oks_delta_identity():
     c = torch.rand(3, 17, 2)
     assert R.oks_delta(c, c) == 0.0
     assert R.oks_delta(c, c + 0.01) > 0.0
+
+
+def test_oracle_yolo_raw_frames_matches_reference(state_dict):
+    """Config-2 micro-bench variant: the reference's yolo_face.yolo on raw
+    640x640 frames (A = 8400, oracle/make_golden_yolo_raw.py) -- det tensor and, on its tie-free
+    copy, yolopt NMS -- against the oracle."""
+    g = _load("golden_yolo_raw.npz")
+    x = synth.frames(2)
+    assert float(x.double().sum()) == pytest.approx(float(g["input_sum"]), rel=0, abs=1e-6)
+    with torch.no_grad():
+        det = R.yolo_net(state_dict, "yolo_face", x, [8.0, 16.0, 32.0])
+    assert det.shape == (2, 5, 8400)
+    assert np.abs(det.numpy() - g["det"]).max() <= 1e-5
+    dets = R.non_max_suppression(torch.from_numpy(g["det_tiefree"]))
+    for i, d in enumerate(dets):
+        n = int(g["nms_count"][i])
+        assert d.shape[0] == n
+        np.testing.assert_array_equal(d.numpy(), g["nms_out"][i, :n])
