@@ -604,6 +604,73 @@ __global__ __launch_bounds__(256) void psa_attention_kernel(prpe_view qkv, prpe_
   }
 }
 
+// The same PSA core for token counts whose score matrix does not fit LDS (the yolopt net on raw
+// 640x640 frames: P5 20x20 = 400 tokens; the config-2 micro-bench variant): one thread per
+// (frame, head, query), keys and values staged through LDS 64 at a time, two passes over the keys
+// (the row maximum, then exp(s - max) and the weighted sum of v), the reference's softmax order
+// of operations (nn.py:115-118: max-subtracted exp, sum, divide) with the same expf. dk <= 32,
+// dh <= 64 (host-checked).
+constexpr int PSA_KC = 64;
+__global__ __launch_bounds__(256) void psa_attention_stream_kernel(prpe_view qkv, prpe_view out, prpe_view vout,
+                                                                   int nh, int dk, int dh, float scale) {
+  __shared__ float Ks[PSA_KC][33];
+  __shared__ float Vs[PSA_KC][65];
+  const int n = blockIdx.x / nh, hd = blockIdx.x - (blockIdx.x / nh) * nh;
+  const int W = qkv.w, L = qkv.h * qkv.w;
+  const int per = 2 * dk + dh;
+  const int i = blockIdx.y * 256 + threadIdx.x;
+  const bool live = i < L;
+  float q[32];
+#pragma unroll
+  for (int d = 0; d < 32; ++d)
+    q[d] = live && d < dk ? qkv.ptr[voff(qkv, n, i / W, i % W, hd * per + d)] : 0.f;
+  auto stage = [&](int j0, bool with_v) {
+    __syncthreads();
+    for (int e = threadIdx.x; e < PSA_KC * 32; e += 256) {
+      const int jj = e / 32, d = e % 32, j = j0 + jj;
+      Ks[jj][d] = j < L && d < dk ? qkv.ptr[voff(qkv, n, j / W, j % W, hd * per + dk + d)] : 0.f;
+    }
+    if (with_v)
+      for (int e = threadIdx.x; e < PSA_KC * 64; e += 256) {
+        const int jj = e / 64, d = e % 64, j = j0 + jj;
+        Vs[jj][d] = j < L && d < dh ? qkv.ptr[voff(qkv, n, j / W, j % W, hd * per + 2 * dk + d)] : 0.f;
+      }
+    __syncthreads();
+  };
+  auto score = [&](int jj) {
+    float a = 0.f;
+    for (int d = 0; d < dk; ++d) a += q[d] * Ks[jj][d];
+    return a * scale;
+  };
+  float m = -INFINITY;
+  for (int j0 = 0; j0 < L; j0 += PSA_KC) {
+    stage(j0, false);
+    const int nj = L - j0 < PSA_KC ? L - j0 : PSA_KC;
+    for (int jj = 0; jj < nj; ++jj) m = fmaxf(m, score(jj));
+  }
+  float sum = 0.f, o[64];
+#pragma unroll
+  for (int d = 0; d < 64; ++d) o[d] = 0.f;
+  for (int j0 = 0; j0 < L; j0 += PSA_KC) {
+    stage(j0, true);
+    const int nj = L - j0 < PSA_KC ? L - j0 : PSA_KC;
+    for (int jj = 0; jj < nj; ++jj) {
+      const float pexp = expf(score(jj) - m);
+      sum += pexp;
+#pragma unroll
+      for (int d = 0; d < 64; ++d) o[d] += pexp * Vs[jj][d];
+    }
+  }
+  if (!live) return;
+#pragma unroll
+  for (int d = 0; d < 64; ++d) {
+    if (d >= dh) break;
+    out.ptr[voff(out, n, i / W, i % W, hd * dh + d)] = o[d] / sum;
+    if (vout.ptr)
+      vout.ptr[voff(vout, n, i / W, i % W, hd * dh + d)] = qkv.ptr[voff(qkv, n, i / W, i % W, hd * per + 2 * dk + d)];
+  }
+}
+
 int attention_launch(const float* qkv, AttnStrides sd, float* out, int32_t B, int32_t L, int32_t H, int32_t D,
                      float scale, int out_planes, void* stream) {
   if (!qkv || !out || B <= 0 || H <= 0 || L != AL || D != AD) return PRPE_EINVAL;
@@ -665,11 +732,16 @@ extern "C" int prpe_psa_attention(const prpe_view* qkv, const prpe_view* out, co
   if (qkv->c != nh * (2 * dk + dh) || out->c != nh * dh || qkv->n != out->n) return PRPE_EINVAL;
   const int L = qkv->h * qkv->w;
   const size_t shm = sizeof(float) * (size_t)nh * L * L;
-  if (shm > 64 * 1024) return PRPE_EINVAL;
   prpe_view vo{};
   if (vout && vout->ptr) {
     if (vout->c != out->c || vout->n != out->n || vout->h != out->h || vout->w != out->w) return PRPE_EINVAL;
     vo = *vout;
+  }
+  if (shm > 64 * 1024) {                   // scores do not fit LDS: the streaming form
+    if (dk > 32 || dh > 64 || (int64_t)qkv->n * nh >= (1LL << 31)) return PRPE_EINVAL;
+    hipLaunchKernelGGL(psa_attention_stream_kernel, dim3(qkv->n * nh, (L + 255) / 256), dim3(256), 0,
+                       as_stream(stream), *qkv, *out, vo, nh, dk, dh, scale);
+    return launch_status();
   }
   hipLaunchKernelGGL(psa_attention_kernel, dim3(qkv->n), dim3(256), shm, as_stream(stream), *qkv, *out, vo, nh, dk,
                      dh, scale);

@@ -32,6 +32,7 @@ namespace {
 
 constexpr int HBK = 32;
 
+
 // 16-row slab GEMM of the epilogue: zc[jn] (16 x 16, jn < NTN) = slab[16][K] x W^T, W held as
 // two bf16 planes (row stride ws, plane stride ps) in LDS; A split into two planes here; three
 // products (precision 0). Lane layout as the main loop's 16x16x32 MFMA.
@@ -110,7 +111,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   unsigned char* const halo0 = lds;
   unsigned char* const ring = lds + 2 * HALO;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the wave index through readfirstlane: provably wave-uniform, so the buffer descriptors and
+  // LDS-DMA destinations derived from it stay in SGPRs (no waterfall loops around the loads)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int fr = lane & 15, fg = lane >> 4;
   int L = xcd_remap(blockIdx.x, p.nwg);
@@ -123,37 +126,55 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   const int n0 = tile_n * BN;
   const int oh0 = th * TR, ow0 = tw * TC;
 
-  // ---- halo DMA: piece q = pixels 8q .. 8q+7 (lane -> pixel 8q + lane/8, physical slot lane%8)
+  // ---- LDS-DMA by buffer loads: every address is a wave-uniform descriptor + a per-lane byte
+  // offset computed ONCE here + a wave-uniform step offset (soffset), so issuing a piece in the
+  // K-loop costs no VALU (the 64-bit address arithmetic per piece and step was ~40 % of the
+  // loop's VALU). Padding pixels get an offset past the descriptor's range: the hardware
+  // returns zeros for them (no branch to a zero page).
+  constexpr unsigned OOB = 0x80000000u;                // > num_records (host-checked < 2^31)
   const float* xn = p.x + (int64_t)n * p.xsn;
-  auto halo_src = [&](int q, int c) -> const float* {
+  const int frame_bytes = (int)(((int64_t)(p.Hi - 1) * p.xsh + (int64_t)(p.Wi - 1) * p.xsw + p.Ci) * 4);
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(xn, frame_bytes);
+  // halo piece q = pixels 8q .. 8q+7 (lane -> pixel 8q + lane/8, physical slot lane%8); this
+  // wave's pieces are q = wave + k NW, k < KQ
+  constexpr int KQ = (HQ + NW - 1) / NW;
+  unsigned hvo[KQ];
+#pragma unroll
+  for (int k = 0; k < KQ; ++k) {
+    const int q = wave + k * NW;
     const int px = q * 8 + (lane >> 3);
     const int hr = px / HW_, hc = px - hr * HW_;
     const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-    const int s = (lane & 7) ^ ((px >> 1) & 7);       // logical slot stored at this lane's slot
-    if (px >= HP || (unsigned)ih >= (unsigned)p.Hi || (unsigned)iw >= (unsigned)p.Wi) return p.zero;
-    return xn + (int64_t)ih * p.xsh + (int64_t)iw * p.xsw + c * HBK + s * 4;
-  };
-  auto issue_halo = [&](int q, int c, int buf) {
-    glds16(halo_src(q, c), halo0 + buf * HALO + q * 1024);
+    const int sl = (lane & 7) ^ ((px >> 1) & 7);      // logical slot stored at this lane's slot
+    const bool ok = q < HQ && px < HP && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
+    hvo[k] = ok ? (unsigned)(((int64_t)ih * p.xsh + (int64_t)iw * p.xsw + sl * 4) * 4) : OOB;
+  }
+  auto issue_halo = [&](int k, int c, int buf) {
+    bl_lds16(xr, halo0 + buf * HALO + (wave + k * NW) * 1024, hvo[k], c * HBK * 4);
   };
 
   // ---- B pieces (as conv_wave.hip): piece j -> plane j / TN, rows 16 (j % TN) .. +16
-  const uint16_t* bsrc[IB];
+  const int wbytes = p.k_pad * 2 * (p.tiles_n * BN);    // one plane [co_pad][k_pad] bf16 / f16
+  const __amdgpu_buffer_rsrc_t wr0 = buf_rsrc(F16 ? p.wh16 : p.whi, wbytes);
+  const __amdgpu_buffer_rsrc_t wr1 = buf_rsrc(F16 ? p.wl16 : p.wlo, wbytes);
+  unsigned bvo[IB];
   int bdst[IB];
+  bool bpl[IB];
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     const int j = wave * IB + i;
     const int q = j / (BN / 16), rb = j % (BN / 16);
     const int nrow = rb * 16 + (lane >> 2);
     const int ch = (lane & 3) ^ swzF(nrow);
-    const uint16_t* plane = F16 ? (q == 0 ? p.wh16 : p.wl16) : (q == 0 ? p.whi : p.wlo);
-    bsrc[i] = plane + (int64_t)(n0 + nrow) * p.k_pad + ch * 8;
+    bvo[i] = (unsigned)(((n0 + nrow) * p.k_pad + ch * 8) * 2);
     bdst[i] = (q * BN + rb * 16) * 64;
+    bpl[i] = q != 0;                                   // wave-uniform
   }
   auto issue_b = [&](int kt, int stage) {
     unsigned char* sb = ring + stage * B_STAGE;
 #pragma unroll
-    for (int i = 0; i < IB; ++i) glds16(bsrc[i] + (int64_t)kt * HBK, sb + bdst[i]);
+    for (int i = 0; i < IB; ++i)
+      bl_lds16(bpl[i] ? wr1 : wr0, sb + bdst[i], bvo[i], kt * HBK * 2);
   };
 
   // precision 3: one frame per block -> one activation scale
@@ -165,12 +186,21 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   }
 
   // A fragment rows of this lane: row block rb = wave * TM + i -> tile row rb / (TC/16),
-  // pixels (rb % (TC/16)) * 16 + fr; halo pixel of tap (kh, kw) = base + kh * HW_ + kw
-  int hbase[TM];
+  // pixels (rb % (TC/16)) * 16 + fr; halo pixel of tap (kh, kw) = base + kh * HW_ + kw. The
+  // byte offset of the first 16-B slot (channels 8 fg .. +3) of every (row block, tap) is
+  // computed once (the tap loop is unrolled); the second slot (+4 .. +7) is logical slot 2 fg + 1
+  // = the first one's physical slot XOR 1, i.e. offset ^ 16
+  int aoff[TM][9];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int rb = wm * TM + i;
-    hbase[i] = (rb / (TC / 16)) * HW_ + (rb % (TC / 16)) * 16 + fr;
+    const int hb0 = (rb / (TC / 16)) * HW_ + (rb % (TC / 16)) * 16 + fr;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int px = hb0 + (t / 3) * HW_ + t % 3;
+      const int sw = (px >> 1) & 7;
+      aoff[i][t] = px * 128 + (((2 * fg) ^ sw) << 4);
+    }
   }
 
   f32x4 acc[TM][TNW];
@@ -182,30 +212,32 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   const int nc = p.Ci / HBK;
   const int nk = nc * 9;
   // prologue: the whole halo of chunk 0 and B(0)
-  for (int q = wave; q < HQ; q += NW) issue_halo(q, 0, 0);
+#pragma unroll
+  for (int k = 0; k < KQ; ++k)
+    if (wave + k * NW < HQ) issue_halo(k, 0, 0);
   issue_b(0, 0);
 
-  int kt = 0;
+#pragma unroll 1
   for (int c = 0; c < nc; ++c) {
     const unsigned char* hb = halo0 + (c & 1) * HALO;
-#pragma unroll 1
-    for (int t = 0; t < 9; ++t, ++kt) {
+    const int kt0 = c * 9;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int kt = kt0 + t;
       wait_barrier<0>();
       if (kt + 1 < nk) issue_b(kt + 1, (kt + 1) & 1);
       if (c + 1 < nc) {
-        // this wave's halo share of chunk c+1 (more than 9 * NW pieces: several per tap)
-        for (int q = t * NW + wave; q < HQ; q += 9 * NW) issue_halo(q, c + 1, (c + 1) & 1);
+        // this wave's halo share of chunk c+1, spread over the taps of chunk c
+#pragma unroll
+        for (int k = t; k < KQ; k += 9)
+          if (wave + k * NW < HQ) issue_halo(k, c + 1, (c + 1) & 1);
       }
-      const int kh = t / 3, kw = t - kh * 3;
       // A fragments: 8 channels (two 16-B slots) of the tap-shifted pixel
       frag_t af[NP][TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int px = hbase[i] + kh * HW_ + kw;
-        const int sw = (px >> 1) & 7;
-        const unsigned char* pp = hb + px * 128;
-        const f4 v0 = *reinterpret_cast<const f4*>(pp + (((2 * fg) ^ sw) << 4));
-        const f4 v1 = *reinterpret_cast<const f4*>(pp + (((2 * fg + 1) ^ sw) << 4));
+        const f4 v0 = *reinterpret_cast<const f4*>(hb + aoff[i][t]);
+        const f4 v1 = *reinterpret_cast<const f4*>(hb + (aoff[i][t] ^ 16));
         if constexpr (APL) {
           af[0][i] = __builtin_bit_cast(bf16x8, v0);
           af[1][i] = __builtin_bit_cast(bf16x8, v1);
@@ -444,9 +476,13 @@ bool conv_halo_eligible(const ConvK& kp, int prec, int km) {
   // 3x3 / stride 1 / pad 1 over whole 32-channel chunks (chunk-major weights), vectorised
   // epilogue, precision 0 (fp32 or planes input) or 3 (fp16 planes + the input's max bound)
   const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.x_planes;
+  // buffer descriptors: one frame of x and one weight plane each < 2^31 bytes (32-bit offsets)
+  const int64_t frame_bytes = ((int64_t)(kp.Hi - 1) * kp.xsh + (int64_t)(kp.Wi - 1) * kp.xsw + kp.Ci) * 4;
+  const int64_t w_bytes = (int64_t)kp.k_pad * 2 * (((kp.Co + 127) / 128) * 128);
   return km == 2 && kp.KH == 3 && kp.KW == 3 && kp.stride == 1 && kp.pad == 1 && kp.Ci % HBK == 0 &&
          kp.vec_out && (prec == 0 || p3) && !kp.in_scale && !kp.x2 && kp.k_pad == kp.K && kp.zero &&
-         kp.Hi == kp.Ho && kp.Wi == kp.Wo;
+         kp.Hi == kp.Ho && kp.Wi == kp.Wo && kp.xsh >= 0 && kp.xsw >= 0 && frame_bytes < (1LL << 31) &&
+         w_bytes < (1LL << 31);
 }
 
 // Where the automatic choice takes it (measured in the model at bs = 256, r02_layer_profile_halo.txt):

@@ -67,16 +67,22 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   static_assert(STAGES == 2 || STAGES == 3, "stages");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave index through readfirstlane: provably uniform, so the descriptors and LDS-DMA
+  // destinations derived from it stay scalar (no waterfall loops around the buffer loads)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
   const int L = xcd_remap(blockIdx.x, p.nwg);
   const int tile_m = L / p.tiles_n, tile_n = L % p.tiles_n;
   const int n0 = tile_n * BN;
   const int wrow0 = tile_m * BM + wave * WTM;
 
-  // ---- A rows of this lane: wrow0 + 16 i + fr; element offset of tap (0,0) at channel 8 fg
-  int64_t rbase[TM];
-  int64_t rbase2[DUAL ? TM : 1];
+  // ---- A rows of this lane: wrow0 + 16 i + fr. The activation operand is read through buffer
+  // descriptors based at the wave's first frame (shifted back by the padding, so every byte
+  // offset is >= 0): rv[i] = the row's offset of tap (0,0) at channel 8 fg, the K-step's tap and
+  // chunk offset is the wave-uniform soffset, and rows past M or taps in the padding read zeros
+  // (an offset past the descriptor's range). No 64-bit address arithmetic per load.
+  unsigned rv[TM];
+  unsigned rv2[DUAL ? TM : 1];
   unsigned hmask[TM], wmask[TM];
   float sa[F16 ? TM : 1];                             // precision 3: per-row (= per-frame) scale
   // A wave's rows [wrow0, wrow0 + WTM) start in frame nf0 and, when a frame holds at least WTM
@@ -92,12 +98,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       if (nb < p.M) am1 = DUAL ? fmaxf(p.x_amax[nf0 + 1], p.x2_amax[nf0 + 1]) : p.x_amax[nf0 + 1];
     }
   }
+  const __amdgpu_buffer_rsrc_t xr =
+      buf_rsrc(p.x + ((int64_t)nf0 * p.xsn - (int64_t)p.pad * (p.xsh + p.xsw)), 0x7FFFFFF0);
+  __amdgpu_buffer_rsrc_t x2r = xr;
+  if constexpr (DUAL) x2r = buf_rsrc(p.x2 + (int64_t)nf0 * p.x2sn, 0x7FFFFFF0);
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = wrow0 + i * 16 + fr;
     unsigned hm = 0, wmk = 0;
-    int64_t b = 0;
-    if constexpr (DUAL) rbase2[i] = 0;
+    unsigned v = BL_OOB, v2 = BL_OOB;
     if constexpr (F16) sa[i] = 1.f;
     if (m < p.M) {
       const int n = m / p.HoWo;
@@ -112,19 +121,26 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       const int oh = rem / p.Wo;
       const int ow = rem - oh * p.Wo;
       const int ih = oh * p.stride - p.pad, iw = ow * p.stride - p.pad;
-      b = (int64_t)n * p.xsn + (int64_t)ih * p.xsh + (int64_t)iw * p.xsw + fg * 8;
-      if constexpr (DUAL) rbase2[i] = (int64_t)n * p.x2sn + (int64_t)oh * p.x2sh + (int64_t)ow * p.x2sw + fg * 8;
+      v = (unsigned)(((int64_t)(n - nf0) * p.xsn + (int64_t)(ih + p.pad) * p.xsh + (int64_t)(iw + p.pad) * p.xsw +
+                      fg * 8) * 4);
+      if constexpr (DUAL)
+        v2 = (unsigned)(((int64_t)(n - nf0) * p.x2sn + (int64_t)oh * p.x2sh + (int64_t)ow * p.x2sw + fg * 8) * 4);
       for (int t = 0; t < p.KH; ++t) hm |= (unsigned)((unsigned)(ih + t) < (unsigned)p.Hi) << t;
       for (int t = 0; t < p.KW; ++t) wmk |= (unsigned)((unsigned)(iw + t) < (unsigned)p.Wi) << t;
     }
-    rbase[i] = b;
+    rv[i] = v;
+    if constexpr (DUAL) rv2[i] = v2;
     hmask[i] = hm;
     wmask[i] = wmk;
   }
 
-  // ---- B pieces: piece j -> plane j / (BN/16), rows 16 (j % (BN/16)) .. +16; lane -> (row, slot)
-  const uint16_t* bsrc[IB];
+  // ---- B pieces: piece j -> plane j / (BN/16), rows 16 (j % (BN/16)) .. +16; lane -> (row, slot),
+  // through one descriptor per plane (the K-step's 64 B as soffset)
+  const int wbytes = p.k_pad * 2 * (p.tiles_n * BN);
+  const uint16_t* planes[3] = {F16 ? p.wh16 : p.whi, F16 ? p.wl16 : p.wlo, p.wlo2};
+  unsigned bvo[IB];
   int bdst[IB];
+  int bq[IB];
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
     int j = wave * IB + i;
@@ -132,19 +148,28 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     const int q = j / (BN / 16), rb = j % (BN / 16);
     const int nrow = rb * 16 + (lane >> 2);
     const int ch = (lane & 3) ^ swzF(nrow);
-    const uint16_t* plane = F16 ? (q == 0 ? p.wh16 : p.wl16) : (q == 0 ? p.whi : (q == 1 ? p.wlo : p.wlo2));
-    bsrc[i] = plane + (int64_t)(n0 + nrow) * p.k_pad + ch * 8;
+    bvo[i] = (unsigned)(((n0 + nrow) * p.k_pad + ch * 8) * 2);
     bdst[i] = (q * BN + rb * 16) * 64;
+    bq[i] = q;                                          // wave-uniform
   }
+  __amdgpu_buffer_rsrc_t wr[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) wr[q] = buf_rsrc(planes[q], wbytes);
   auto issue_b = [&](int kt, int stage) {
     unsigned char* sb = lds + stage * B_STAGE;
 #pragma unroll
-    for (int i = 0; i < IB; ++i) glds16(bsrc[i] + (int64_t)kt * BK, sb + bdst[i]);
+    for (int i = 0; i < IB; ++i) {
+      __amdgpu_buffer_rsrc_t r = wr[0];
+#pragma unroll
+      for (int q = 1; q < NP; ++q)
+        if (bq[i] == q) r = wr[q];
+      bl_lds16(r, sb + bdst[i], bvo[i], kt * BK * 2);
+    }
   };
 
   // ---- A walk (wave-uniform): k = ((ci/32)*KH*KW + kh*KW + kw)*32 + ci%32
   int u_kh = 0, u_kw = 0, u_ci = 0, u_step = 0;
-  int64_t u_off = 0;                                  // kh*xsh + kw*xsw + chunk*32
+  int u_off = 0;                                      // kh*xsh + kw*xsw + chunk*32 (elements)
   const int nk = p.nk;
   f4 raw[TM][2];
   unsigned amask = 0;
@@ -161,21 +186,28 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const bool ok = (hmask[i] >> u_kh) & (wmask[i] >> u_kw) & 1u;
-      const float* src;
-      if constexpr (DUAL)
-        src = !ok ? p.zero : (second ? p.x2 + (rbase2[i] + (u_off - (int64_t)p.nk1 * BK)) : p.x + (rbase[i] + u_off));
-      else
-        src = ok ? p.x + (rbase[i] + u_off) : p.zero;
-      raw[i][0] = *reinterpret_cast<const f4*>(src);
-      raw[i][1] = *reinterpret_cast<const f4*>(src + 4);
+      if constexpr (DUAL) {
+        if (second) {                                   // x2: 1x1, never padded
+          const int so = (u_off - p.nk1 * BK) * 4;
+          raw[i][0] = bl_f4(x2r, rv2[i], so);
+          raw[i][1] = bl_f4(x2r, rv2[i] + 16, so);
+        } else {
+          raw[i][0] = bl_f4(xr, rv[i], u_off * 4);
+          raw[i][1] = bl_f4(xr, rv[i] + 16, u_off * 4);
+        }
+      } else {
+        const unsigned v = ok ? rv[i] : BL_OOB;
+        raw[i][0] = bl_f4(xr, v, u_off * 4);
+        raw[i][1] = bl_f4(xr, v + 16, u_off * 4);
+      }
       if constexpr (PRO) amask |= (unsigned)ok << i;
     }
     // advance to the next K-step (kw, then kh, then the next chunk); stay on the last one
     if (++u_step < nk) {
-      u_off += p.xsw;
+      u_off += (int)p.xsw;
       if (++u_kw == p.KW) {
-        u_kw = 0; u_off += p.xsh - (int64_t)p.KW * p.xsw;
-        if (++u_kh == p.KH) { u_kh = 0; u_ci += BK; u_off += BK - (int64_t)p.KH * p.xsh; }
+        u_kw = 0; u_off += (int)(p.xsh - (int64_t)p.KW * p.xsw);
+        if (++u_kh == p.KH) { u_kh = 0; u_ci += BK; u_off += (int)(BK - (int64_t)p.KH * p.xsh); }
       }
     } else {
       u_step = nk - 1;
@@ -418,8 +450,17 @@ bool conv_wave_eligible(const ConvK& kp, int prec, int km) {
   const bool chunked = km == 2 || (km == 1 && kp.KH * kp.KW == 1 && kp.Ci % 32 == 0);
   const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.in_scale && (!kp.x2 || kp.x2_amax);
   const bool planes_ok = !kp.x_planes || (prec == 0 && !kp.in_scale && !kp.x2);
+  // buffer descriptors: a wave's rows (at most 64, spanning at most 64 / HoWo + 2 frames) and its
+  // taps must lie within 2^31 bytes of the wave's first frame, with non-negative strides
+  const int64_t span_f = 64 / kp.HoWo + 2;
+  const int64_t x_span = (span_f * kp.xsn + (int64_t)(kp.KH + kp.pad) * kp.xsh + (int64_t)(kp.KW + kp.pad) * kp.xsw +
+                          kp.Ci) * 4;
+  const int64_t x2_span = kp.x2 ? (span_f * kp.x2sn + (int64_t)kp.Ho * kp.x2sh + (int64_t)kp.Wo * kp.x2sw + 64) * 4 : 0;
+  const bool addr_ok = kp.xsn >= 0 && kp.xsh >= 0 && kp.xsw >= 0 && x_span < 0x7FFFFFF0LL &&
+                       (!kp.x2 || (kp.x2sn >= 0 && kp.x2sh >= 0 && kp.x2sw >= 0 && x2_span < 0x7FFFFFF0LL)) &&
+                       (int64_t)kp.k_pad * 2 * kp.Co < (1LL << 30);
   return chunked && kp.vec_out && (prec == 0 || prec == 2 || p3) && kp.K % BK == 0 && kp.k_pad == kp.K &&
-         kp.zero != nullptr && planes_ok;
+         kp.zero != nullptr && planes_ok && addr_ok;
 }
 
 // tile 20 = auto; 21.. force a configuration (tools/conv_bench.py sweeps them)

@@ -1030,20 +1030,24 @@ def test_vit_attention_head_major_operand_bit_identical():
     assert torch.equal(a, b)
 
 
-def test_psa_attention():
+@pytest.mark.parametrize("hw", [5, 20, 17])
+def test_psa_attention(hw):
+    """5x5: the LDS score-matrix kernel (the model's P5 after the adapter); 20x20 (raw 640x640
+    frames, the config-2 micro-bench variant) and 17x17: the streaming two-pass kernel."""
     B, nh, dk, dh = 2, 2, 32, 64
     per = 2 * dk + dh
-    qkv = rnd(B, nh * per, 5, 5, seed=43)
-    out = torch.empty(B, 5, 5, nh * dh, device=DEV)
-    vout = torch.empty(B, 5, 5, nh * dh, device=DEV)
+    L = hw * hw
+    qkv = rnd(B, nh * per, hw, hw, seed=43, scale=2.0)
+    out = torch.empty(B, hw, hw, nh * dh, device=DEV)
+    vout = torch.empty(B, hw, hw, nh * dh, device=DEV)
     ops.psa_attention(qkv.permute(0, 2, 3, 1).contiguous().to(DEV), out, vout, nh, dk, dh, dk ** -0.5)
     torch.cuda.synchronize()
-    t = qkv.view(B, nh, per, 25)
+    t = qkv.view(B, nh, per, L).double()
     q, k, v = t.split([dk, dk, dh], dim=2)
     att = ((q.transpose(-2, -1) @ k) * dk ** -0.5).softmax(-1)
-    ref = (v @ att.transpose(-2, -1)).reshape(B, nh * dh, 5, 5)
+    ref = (v @ att.transpose(-2, -1)).reshape(B, nh * dh, hw, hw).float()
     torch.testing.assert_close(out.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=1e-5)
-    torch.testing.assert_close(vout.permute(0, 3, 1, 2).cpu(), v.reshape(B, nh * dh, 5, 5), rtol=0, atol=0)
+    torch.testing.assert_close(vout.permute(0, 3, 1, 2).cpu(), v.float().reshape(B, nh * dh, hw, hw), rtol=0, atol=0)
 
 
 def test_l2norm():
