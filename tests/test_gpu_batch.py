@@ -137,6 +137,19 @@ def test_config3_bs256_parity_on_spread_frames(model, state_dict):
     assert torch.equal(h2[0], heat[255]) and torch.equal(h2[1], heat[0])
 
 
+def _raw_yolo_close(det, ref):
+    """Tolerances of the raw-frame YOLO. The synthetic net is ill-conditioned on raw 640x640
+    frames (its BN statistics were calibrated on the adapter's output; scores saturate at 1.0):
+    measured on the CPU oracle, fp32 vs fp64 moves a score by 3.1e-4 and a 2^-20 relative
+    perturbation of the YOLO weights by 2.0e-3 (boxes 5e-4 of max). Any fp32 evaluation order
+    lands in that band, so: every score within 4e-3 (2x the 2^-20 response), fewer than 0.1 % of
+    the anchors beyond 1e-3, boxes within 2e-3 x max|box|."""
+    e = (det[:, 4] - ref[:, 4]).abs()
+    assert e.max().item() <= 4e-3, e.max().item()
+    assert (e > 1e-3).float().mean().item() < 1e-3
+    assert (det[:, :4] - ref[:, :4]).abs().max().item() <= 2e-3 * ref[:, :4].abs().max().item()
+
+
 def test_config2_micro_yolo_raw_frames_vs_reference_golden(model):
     """Config-2 micro-bench variant: ``model.yolo_face.yolo(frames)`` -- YOLO
     v11n nc=1 straight on raw 640x640 frames, A = 8400 -- against the reference's own output
@@ -152,8 +165,7 @@ def test_config2_micro_yolo_raw_frames_vs_reference_golden(model):
         model.yolo_face.yolo.head.stride = torch.zeros(3)
     ref = torch.from_numpy(g["det"])
     assert det.shape == ref.shape == (2, 5, 8400)
-    assert (det[:, 4] - ref[:, 4]).abs().max().item() <= 1e-3
-    assert (det[:, :4] - ref[:, :4]).abs().max().item() <= 2e-3 * ref[:, :4].abs().max().item()
+    _raw_yolo_close(det, ref)
     dets, cnt = non_max_suppression_padded(torch.from_numpy(g["det_tiefree"]).cuda())
     assert cnt.cpu().tolist() == g["nms_count"].tolist()
     for i, n in enumerate(g["nms_count"].tolist()):
@@ -170,8 +182,7 @@ def test_config2_micro_yolo_raw_bs64_parity(model, state_dict):
     idx = spread(64)
     with torch.no_grad():
         ref = R.yolo_net(state_dict, "yolo_face", x[idx], STRIDE)
-    assert (det[idx, 4] - ref[:, 4]).abs().max().item() <= 1e-3
-    assert (det[idx, :4] - ref[:, :4]).abs().max().item() <= 2e-3 * ref[:, :4].abs().max().item()
+    _raw_yolo_close(det[idx], ref)
     # frame independence on this path
     d2 = model.engine.yolo_raw("yolo_face", x[[63, 0]].cuda(), STRIDE).cpu()
     assert torch.equal(d2[0], det[63]) and torch.equal(d2[1], det[0])
