@@ -156,10 +156,16 @@ class Engine:
         return t
 
     @staticmethod
-    def _f16_ok(x, p: ConvPack, out):
+    def _vec4(t):
+        """16-B vector rows (the precision-3 kernels' epilogue needs them for y and the residual)."""
+        return t is None or (t.stride(3) == 1 and t.shape[3] % 4 == 0 and t.data_ptr() % 16 == 0 and
+                             all(st % 4 == 0 for st in t.stride()[:3]))
+
+    @staticmethod
+    def _f16_ok(x, p: ConvPack, out, res=None):
         chunked = p.k_order == 1 or (p.kh * p.kw == 1 and p.ci % 32 == 0)
         return (chunked and p.in_scale is None and x.stride(3) == 1 and x.data_ptr() % 16 == 0 and
-                out.shape[3] % 4 == 0 and getattr(x, "_prpe_amax", None) is not None)
+                Engine._vec4(out) and Engine._vec4(res) and getattr(x, "_prpe_amax", None) is not None)
 
     def pk_dual(self, q) -> ConvPack:
         """Bottleneck ``q`` (block 0 of a stage): relu(bn3(conv3(o)) + bn_ds(downsample(x))) as
@@ -190,7 +196,7 @@ class Engine:
         if out is None:
             out = self.empty(B, Ho, Wo, p.co)
         prec = self.precision
-        if prec == 3 and (not self._f16_ok(x, p, out) or (x2 is not None and x2_amax is None)):
+        if prec == 3 and (not self._f16_ok(x, p, out, res) or (x2 is not None and x2_amax is None)):
             prec = 2
         xa = getattr(x, "_prpe_amax", None) if prec == 3 else None
         ya = self.amax_slot(B) if self.precision == 3 and w2 is None else None

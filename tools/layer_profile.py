@@ -41,8 +41,8 @@ def main():
     rows = []
     for name, evs in e.events.items():
         ms = sum(s.elapsed_time(f) for s, f, *_ in evs)
-        fl = sum(2.0 * px * p.co * p.ci * p.kh * p.kw for _, _, px, p, _ in evs)
-        _, _, px, p, prc = evs[0]
+        fl = sum(2.0 * px * p.co * p.ci * p.kh * p.kw for _, _, px, p, *_ in evs)
+        _, _, px, p, prc, *_ = evs[0]
         rows.append((ms, name, len(evs), fl, p, prc, px))
     rows.sort(reverse=True)
     conv_ms = sum(r[0] for r in rows)
