@@ -18,19 +18,38 @@ static inline int launch_status() {
   return e == hipSuccess ? 0 : static_cast<int>(e);
 }
 
+// Elementwise helpers for T = float or f32x2v (two lanes' worth in one VGPR pair: in VALU-bound
+// kernels without MFMAs -- the upconv -- v_pk_fma_f32 / v_pk_mul_f32 issue one instruction per two
+// values). Every multiply-add is an explicit fma and contraction is off, so the float and the
+// f32x2v instantiations round identically (bit-identical results whichever a kernel uses).
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ T vfma(T a, T b, T c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ float vexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ f32x2v vexp2(f32x2v x) {
+  return f32x2v{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])};
+}
+__device__ __forceinline__ float vrcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ f32x2v vrcp(f32x2v x) { return f32x2v{__builtin_amdgcn_rcpf(x[0]), __builtin_amdgcn_rcpf(x[1])}; }
+__device__ __forceinline__ float vsel_lt1(float a, float x, float y) { return a < 1.f ? x : y; }
+__device__ __forceinline__ f32x2v vsel_lt1(f32x2v a, f32x2v x, f32x2v y) {
+  return f32x2v{a[0] < 1.f ? x[0] : y[0], a[1] < 1.f ? x[1] : y[1]};
+}
+
 // exp(x) from the hardware base-2 exponential (v_exp_f32, 1 ulp) with x*log2(e) carried in
 // two parts (t + e), so the argument rounding does not grow with |x|: 2^(t+e) = 2^t (1 + e ln2)
 // to ~2 ulp over the normal range; overflows to +inf and underflows to 0 like expf.
-// 1 + e ln2 is within 2^-20 of 1, so it is finite and positive.
-__device__ __forceinline__ float exp_hw(float x) {
-  const float L = 1.44269502162933349609375f;     // log2(e) rounded to fp32
-  const float Llo = 1.925963033500011e-08f;       // log2(e) - L
-  const float t = x * L;
-  const float e = fmaf(x, L, -t) + x * Llo;
-  // r * (1 + e ln2), not fma(r, e ln2, r): an overflowed r = inf times a correction below 0
-  // would give inf - inf = NaN
-  return __builtin_amdgcn_exp2f(t) * (1.f + e * 0.693147180559945309f);
+// 1 + e ln2 is within 2^-20 of 1, so it is finite and positive; r * (1 + e ln2), not
+// fma(r, e ln2, r): an overflowed r = inf times a correction below 0 would give inf - inf = NaN
+template <typename T>
+__device__ __forceinline__ T exp_hw_v(T x) {
+#pragma clang fp contract(off)
+  const T L = T(1.44269502162933349609375f);     // log2(e) rounded to fp32
+  const T Llo = T(1.925963033500011e-08f);       // log2(e) - L
+  const T t = x * L;
+  const T e = vfma(x, Llo, vfma(x, L, -t));
+  return vexp2(t) * vfma(e, T(0.693147180559945309f), T(1.f));
 }
+__device__ __forceinline__ float exp_hw(float x) { return exp_hw_v<float>(x); }
 
 // erf(x) without branches (both pieces are evaluated; the select is per lane), ~24 VALU
 // instead of libm erff's two-branch form with a full expf (~45 VALU under divergence):
@@ -40,28 +59,44 @@ __device__ __forceinline__ float exp_hw(float x) {
 // least-squares fits made for this kernel (relative error of erf(x)/x, absolute error of
 // log erfc); max error 2.3 ulp over [-6, 6] in an fp32 emulation with exp_hw's 2 ulp, 1.5e-7
 // absolute. test_epilogue_activation_accuracy checks GELU through it against fp64.
-__device__ __forceinline__ float erf_fast(float x) {
-  const float a = fabsf(x);
-  const float t = a * a;
-  float p = -0x1.26eecap-11f;
-  p = fmaf(p, t, 0x1.422d30p-8f);
-  p = fmaf(p, t, -0x1.b59da6p-6f);
-  p = fmaf(p, t, 0x1.ce08bep-4f);
-  p = fmaf(p, t, -0x1.812670p-2f);
-  p = fmaf(p, t, 0x1.20dd74p+0f);
-  const float ra = a * p;
-  const float b = fminf(a, 4.f);
-  float q = 0x1.b14578p-20f;
-  q = fmaf(q, b, -0x1.7e711ep-15f);
-  q = fmaf(q, b, 0x1.36c82ep-11f);
-  q = fmaf(q, b, -0x1.36a7bcp-8f);
-  q = fmaf(q, b, 0x1.aff5a4p-6f);
-  q = fmaf(q, b, -0x1.c2788cp-4f);
-  q = fmaf(q, b, -0x1.438d42p-1f);
-  q = fmaf(q, b, -0x1.21529ap+0f);
-  q = fmaf(q, b, 0x1.3df11ep-12f);
-  const float rb = 1.f - exp_hw(q);
-  return copysignf(a < 1.f ? ra : rb, x);
+template <typename T>
+__device__ __forceinline__ T erf_fast_v(T x) {
+#pragma clang fp contract(off)
+  const T a = __builtin_elementwise_abs(x);
+  const T t = a * a;
+  T p = T(-0x1.26eecap-11f);
+  p = vfma(p, t, T(0x1.422d30p-8f));
+  p = vfma(p, t, T(-0x1.b59da6p-6f));
+  p = vfma(p, t, T(0x1.ce08bep-4f));
+  p = vfma(p, t, T(-0x1.812670p-2f));
+  p = vfma(p, t, T(0x1.20dd74p+0f));
+  const T ra = a * p;
+  const T b = __builtin_elementwise_min(a, T(4.f));
+  T q = T(0x1.b14578p-20f);
+  q = vfma(q, b, T(-0x1.7e711ep-15f));
+  q = vfma(q, b, T(0x1.36c82ep-11f));
+  q = vfma(q, b, T(-0x1.36a7bcp-8f));
+  q = vfma(q, b, T(0x1.aff5a4p-6f));
+  q = vfma(q, b, T(-0x1.c2788cp-4f));
+  q = vfma(q, b, T(-0x1.438d42p-1f));
+  q = vfma(q, b, T(-0x1.21529ap+0f));
+  q = vfma(q, b, T(0x1.3df11ep-12f));
+  const T rb = T(1.f) - exp_hw_v(q);
+  return __builtin_elementwise_copysign(vsel_lt1(a, ra, rb), x);
+}
+__device__ __forceinline__ float erf_fast(float x) { return erf_fast_v<float>(x); }
+
+// GELU and SiLU / sigmoid (the epilogue forms, see apply_act) for T = float or f32x2v
+template <typename T>
+__device__ __forceinline__ T gelu_v(T v) {
+#pragma clang fp contract(off)
+  const T h = T(0.5f) * v;
+  return vfma(h, erf_fast_v(v * T(0.70710678118654752440f)), h);
+}
+template <typename T>
+__device__ __forceinline__ T sigmoid_v(T v) {
+#pragma clang fp contract(off)
+  return vrcp(T(1.f) + exp_hw_v(-v));
 }
 
 // Activation applied in every epilogue, accurate to a few ulp of the fp32 CPU reference:
@@ -70,12 +105,35 @@ __device__ __forceinline__ float erf_fast(float x) {
 __device__ __forceinline__ float apply_act(float v, int act, float slope) {
   switch (act) {
     case PRPE_ACT_RELU: return v > 0.f ? v : 0.f;
-    case PRPE_ACT_SILU: return v * __builtin_amdgcn_rcpf(1.f + exp_hw(-v));
+    case PRPE_ACT_SILU: return v * sigmoid_v(v);
     case PRPE_ACT_PRELU: return v >= 0.f ? v : v * slope;
-    case PRPE_ACT_GELU: return 0.5f * v * (1.f + erf_fast(v * 0.70710678118654752440f));
-    case PRPE_ACT_SIGMOID: return __builtin_amdgcn_rcpf(1.f + exp_hw(-v));
+    case PRPE_ACT_GELU: return gelu_v(v);
+    case PRPE_ACT_SIGMOID: return sigmoid_v(v);
     default: return v;
   }
+}
+
+// the same activation on 4 values, two at a time in packed fp32 (VALU-only kernels: the
+// upconv); bit-identical to apply_act element by element
+__device__ __forceinline__ f32x4 apply_act4(f32x4 v, int act, f32x4 slope) {
+  if (act == PRPE_ACT_GELU || act == PRPE_ACT_SILU || act == PRPE_ACT_SIGMOID) {
+    f32x2v lo = {v[0], v[1]}, hi = {v[2], v[3]};
+    if (act == PRPE_ACT_GELU) {
+      lo = gelu_v(lo);
+      hi = gelu_v(hi);
+    } else if (act == PRPE_ACT_SILU) {
+      lo = lo * sigmoid_v(lo);
+      hi = hi * sigmoid_v(hi);
+    } else {
+      lo = sigmoid_v(lo);
+      hi = sigmoid_v(hi);
+    }
+    return f32x4{lo[0], lo[1], hi[0], hi[1]};
+  }
+  f32x4 r;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) r[q] = apply_act(v[q], act, slope[q]);
+  return r;
 }
 
 // fp32 -> (hi, lo) bf16 pair, hi = RNE(x), lo = RNE(x - hi). |x - hi - lo| <= 2^-17 |x|.
@@ -201,6 +259,19 @@ __device__ __forceinline__ int f16_scale_exp(float amax) {
 }
 
 // F = {0,2,3,1} indexed by (row >> 2) & 3, branch-free
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+// buffer-descriptor LDS-DMA: one piece of 16 B per lane from the descriptor's base + voff + soff
+// (bytes; voff per lane, soff wave-uniform) to dst_lds + 16 * lane (dst wave-uniform). An offset
+// at or past the descriptor's num_records reads zeros (the padding idiom of conv_halo.hip).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int num_bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, num_bytes, 0x00020000);
+}
+__device__ __forceinline__ void bl_lds16(__amdgpu_buffer_rsrc_t r, void* dst_lds, unsigned voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst_lds), 16, voff, soff, 0, 0);
+}
+constexpr unsigned BL_OOB = 0x80000000u;   // a voffset past every descriptor's range (num_records < 2^31)
+
 __device__ __forceinline__ int swzF(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }
 
 // native vector types: HIP's float4/uint4 are structs, and arrays of them cannot be promoted

@@ -95,7 +95,6 @@ __device__ __forceinline__ void split_planes_f16(f4 v, float sa, unsigned long l
   for (int q = 0; q < 2; ++q) pl[q] = (unsigned long long)u[q][0] | ((unsigned long long)u[q][1] << 32);
 }
 
-typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 // one LDS-DMA piece: 16 B per lane from src (per lane) to dst_lds + 16 * lane (dst wave-uniform)
@@ -103,22 +102,11 @@ __device__ __forceinline__ void glds16(const void* src, void* dst_lds) {
   __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src), (lds_ptr_t)(dst_lds), 16, 0, 0);
 }
 
-// buffer-descriptor LDS-DMA: one piece of 16 B per lane from the descriptor's base + voff + soff
-// (bytes; voff per lane, soff wave-uniform) to dst_lds + 16 * lane (dst wave-uniform). An offset
-// at or past the descriptor's num_records reads zeros (the padding idiom of conv_halo.hip).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int num_bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, num_bytes, 0x00020000);
-}
-__device__ __forceinline__ void bl_lds16(__amdgpu_buffer_rsrc_t r, void* dst_lds, unsigned voff, int soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst_lds), 16, voff, soff, 0, 0);
-}
-
 // 16 B per lane into registers through a buffer descriptor (base + voff + soff, bytes); zeros
 // at or past num_records
 __device__ __forceinline__ f4 bl_f4(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
-constexpr unsigned BL_OOB = 0x80000000u;   // a voffset past every descriptor's range (num_records < 2^31)
 
 // s_waitcnt vmcnt(N) + s_barrier in one asm statement with a memory clobber: no LDS access
 // may be moved across it, and it does not drain the LDS-DMA copies still in flight (a

@@ -201,8 +201,17 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
       for (int v = 0; v < VW; ++v) acc[v] = lerp_add(acc[v], ly, hA[dy][v], hB[dy][v]);
     }
     float out[VW];
+    if constexpr (VW == 4) {
+      f32x4 pre;
 #pragma unroll
-    for (int v = 0; v < VW; ++v) out[v] = apply_act(acc[v] * sc[v] + bi[v], ACT >= 0 ? ACT : p.act, sl[v]);
+      for (int v = 0; v < 4; ++v) pre[v] = acc[v] * sc[v] + bi[v];
+      const f32x4 o4 = apply_act4(pre, ACT >= 0 ? ACT : p.act, f32x4{sl[0], sl[1], sl[2], sl[3]});
+#pragma unroll
+      for (int v = 0; v < 4; ++v) out[v] = o4[v];
+    } else {
+#pragma unroll
+      for (int v = 0; v < VW; ++v) out[v] = apply_act(acc[v] * sc[v] + bi[v], ACT >= 0 ? ACT : p.act, sl[v]);
+    }
     float* y = yn + (int64_t)oy * p.y.sh + yo;
     if constexpr ((ABL & 2) != 0) {
       if (out[0] + out[VW - 1] == 12345.678f) y[0] = out[0];
@@ -223,6 +232,200 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
     }
 #pragma unroll
     for (int v = 0; v < VW; ++v) y[(int64_t)v * p.y.sc] = out[v];
+  }
+}
+
+// LDS-DMA form (round 3; the automatic choice for VW = 4 whenever its geometry rules hold). Why:
+// gfx950 has one vmcnt for a wave's loads AND stores, so in the fused kernel every H-row reload
+// (6 dependent L2 loads per tap row, ~once per source interval) also waits for the output
+// stores issued before it: loads and stores serialise (diagnostic builds: no loads 0.88 ms, no
+// stores 0.84, full 1.56 at the face-YOLO shape, bs = 64). Here the z rows reach LDS by
+// buffer-descriptor LDS-DMA, one source row ahead, issued right after the block barrier that
+// brings the previous row into use: by the time a row is read, at least UPD_MIN stores (output
+// rows x stores per row) were issued after its DMA, so `vmcnt(that many)` covers the DMA and
+// never the recent stores. The H rows and the output follow the fused kernel's arithmetic
+// exactly (same lerp_add sequence, same epilogue): bit-identical results.
+// Block: frame n, output rows [oy0, oy1), 32 output columns x 32 channels (thread = 4 channels of
+// one column; 8 threads = one pixel's 128-B line, so a wave stores 8 full lines), the source
+// window of the block's columns (at most UPD_NSC source columns) x 9 taps x 32 channels per
+// source row in a ring of UPD_RING rows (128-B segments, 8 lanes per segment).
+constexpr int UPD_W = 32, UPD_C = 32, UPD_NSC = 8, UPD_RING = 4;
+constexpr int UPD_SEG = UPD_NSC * 9;                  // 128-B segments per source row
+constexpr int UPD_NI = (UPD_SEG + 7) / 8;             // 1-KiB DMA instructions per source row
+constexpr int UPD_MIN = 4;                            // output rows between a row's DMA and its use
+
+template <int ACT, bool PL>
+__global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rblocks, int ctiles, int cblocks) {
+  __shared__ __attribute__((aligned(1024))) float ring[UPD_RING][UPD_NI * 256];
+  __shared__ int ty0[UP_MAX_R + 2];
+  __shared__ float tly[UP_MAX_R + 2];
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  int t = bid;
+  const int cb = t % cblocks;
+  t /= cblocks;
+  const int ct = t % ctiles;
+  t /= ctiles;
+  const int rbk = t % rblocks;
+  const int n = t / rblocks;
+  const int Ho = p.y.h, Hi = p.z.h, Wo = p.y.w, Wi = p.z.w;
+  const int oy0 = rbk * R, oy1 = oy0 + R < Ho ? oy0 + R : Ho;
+  const int ox0 = ct * UPD_W, c0 = cb * UPD_C;
+  for (int e = threadIdx.x; e < oy1 - oy0 + 2; e += 256) {
+    const int yy = oy0 - 1 + e;
+    int y0 = -1, y1;
+    float ly = 0.f;
+    if ((unsigned)yy < (unsigned)Ho) bilin_src(yy, Hi, Ho, p.ac, y0, y1, ly);
+    ty0[e] = y0;
+    tly[e] = ly;
+  }
+  // source column window of the block (host-checked to span <= UPD_NSC columns)
+  int xs_lo, xs_hi, tmp;
+  float ltmp;
+  bilin_src(ox0 > 0 ? ox0 - 1 : 0, Wi, Wo, p.ac, xs_lo, tmp, ltmp);
+  bilin_src(ox0 + UPD_W < Wo ? ox0 + UPD_W : Wo - 1, Wi, Wo, p.ac, tmp, xs_hi, ltmp);
+  const int nsc = xs_hi - xs_lo + 1;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // DMA: segment s = (source column j, tap) -> 128 B = channels c0 .. c0+31 of that tap map;
+  // instruction i of a row moves segments 8i .. 8i+7 (lane -> segment 8i + lane/8, 16 B each)
+  const float* zn = p.z.ptr + (int64_t)n * p.z.sn;
+  const int zbytes = (int)(((int64_t)(Hi - 1) * p.z.sh + (int64_t)(Wi - 1) * p.z.sw + 9 * p.Co) * 4);
+  const __amdgpu_buffer_rsrc_t zr = buf_rsrc(zn, zbytes);
+  unsigned dvo[(UPD_NI + 3) / 4];
+#pragma unroll
+  for (int k = 0; k < (UPD_NI + 3) / 4; ++k) {
+    const int i = wave + 4 * k;
+    const int sg = i * 8 + (lane >> 3);
+    const int j = sg / 9, tp = sg - j * 9;
+    dvo[k] = (i < UPD_NI && j < nsc)
+                 ? (unsigned)((((int64_t)(xs_lo + j) * p.z.sw + tp * p.Co + c0) + (lane & 7) * 4) * 4)
+                 : BL_OOB;
+  }
+  auto issue_row = [&](int r) {
+#pragma unroll
+    for (int k = 0; k < (UPD_NI + 3) / 4; ++k) {
+      const int i = wave + 4 * k;
+      if (i < UPD_NI)
+        bl_lds16(zr, reinterpret_cast<unsigned char*>(ring[r % UPD_RING]) + i * 1024, dvo[k],
+                 (int)((int64_t)r * p.z.sh * 4));
+    }
+  };
+
+  // this thread: output column ox, channels c0 + 4 cg .. +3
+  const int col = tid >> 3, cg = tid & 7;
+  const int ox = ox0 + col;
+  const bool live = ox < Wo;                          // Co % 32 == 0 (host-checked)
+  const bool wlive = __builtin_amdgcn_ballot_w64(live) != 0;   // wave-uniform
+  int lo[3], l1[3];
+  float lx[3];
+  unsigned xvalid = 0;
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int xx = ox + dx - 1;
+    int x0 = xs_lo, x1 = xs_lo;
+    float l = 0.f;
+    if (live && (unsigned)xx < (unsigned)Wo) {
+      bilin_src(xx, Wi, Wo, p.ac, x0, x1, l);
+      xvalid |= 1u << dx;
+    }
+    // float offset of (column, tap dy = 0, dx) in a ring row; the tap row dy adds 3 dy segments
+    lo[dx] = ((x0 - xs_lo) * 9 + dx) * 32 + cg * 4;
+    l1[dx] = ((x1 - xs_lo) * 9 + dx) * 32 + cg * 4;
+    lx[dx] = l;
+  }
+  float sc[4], bi[4], sl[4];
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    const int c = c0 + cg * 4 + v;
+    sc[v] = p.scale ? p.scale[c] : 1.f;
+    bi[v] = p.bias ? p.bias[c] : 0.f;
+    sl[v] = p.slope ? p.slope[c] : 0.f;
+  }
+  auto hrow = [&](int r, int dy, float (&h)[4]) {
+    const float* rr = ring[r % UPD_RING] + dy * 3 * 32;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) h[v] = 0.f;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      if (!((xvalid >> dx) & 1u)) continue;
+      const f32x4 A = *reinterpret_cast<const f32x4*>(rr + lo[dx]);
+      const f32x4 B = *reinterpret_cast<const f32x4*>(rr + l1[dx]);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) h[v] = lerp_add(h[v], lx[dx], A[v], B[v]);
+    }
+  };
+  __syncthreads();                                    // the row tables
+  // rows in use for output row oy: [y0 of row oy-1 (or oy), y1 of row oy+1]; hi_at = the top one
+  auto hi_at = [&](int oy) {
+    int h = -1;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const int y0 = ty0[oy - oy0 + dy];
+      if (y0 >= 0) h = y0 < Hi - 1 ? y0 + 1 : y0;
+    }
+    return h;
+  };
+  int lo_row = Hi;
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int y0 = ty0[dy];
+    if (y0 >= 0 && y0 < lo_row) lo_row = y0;
+  }
+  int issued = __builtin_amdgcn_readfirstlane(hi_at(oy0));
+  for (int r = __builtin_amdgcn_readfirstlane(lo_row); r <= issued; ++r) issue_row(r);
+  if (issued + 1 < Hi) issue_row(++issued);           // one row ahead
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  int in_use = hi_at(oy0);
+
+  const int yo = ox * (int)p.y.sw + (c0 + cg * 4) * (int)p.y.sc;
+  float* yn = p.y.ptr + (int64_t)n * p.y.sn;
+  float hA[3][4], hB[3][4];
+  int cur[3] = {-2, -2, -2};
+  for (int oy = oy0; oy < oy1; ++oy) {
+    const int need = __builtin_amdgcn_readfirstlane(hi_at(oy));
+    if (need > in_use) {
+      // the row(s) coming into use were DMA'd at the previous such event, >= UPD_MIN output rows
+      // (stores) ago: wait for everything older than those stores, then publish every wave's
+      // pieces. A wave with no live column issues no stores: it waits for all of its DMA.
+      if (!wlive) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      else if constexpr (PL) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      in_use = need;
+      while (issued < need + 1 && issued + 1 < Hi) issue_row(++issued);   // one row ahead again
+    }
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy) {
+      const int y0 = __builtin_amdgcn_readfirstlane(ty0[oy - oy0 + dy]);
+      if (y0 < 0) continue;
+      const float ly = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(
+                                                     __builtin_bit_cast(int, tly[oy - oy0 + dy])));
+      const int y1 = y0 < Hi - 1 ? y0 + 1 : y0;
+      if (y0 != cur[dy]) {
+        if (y0 == cur[dy] + 1) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) hA[dy][v] = hB[dy][v];
+        } else {
+          hrow(y0, dy, hA[dy]);
+        }
+        hrow(y1, dy, hB[dy]);
+        cur[dy] = y0;
+      }
+#pragma unroll
+      for (int v = 0; v < 4; ++v) acc[v] = lerp_add(acc[v], ly, hA[dy][v], hB[dy][v]);
+    }
+    if (!live) continue;
+    f32x4 pre;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) pre[v] = acc[v] * sc[v] + bi[v];
+    const f32x4 o4 = apply_act4(pre, ACT >= 0 ? ACT : p.act, f32x4{sl[0], sl[1], sl[2], sl[3]});
+    const float out[4] = {o4[0], o4[1], o4[2], o4[3]};
+    float* y = yn + (int64_t)oy * p.y.sh + yo;
+    if constexpr (PL)
+      store_planes4<true>(reinterpret_cast<uint16_t*>(y - (c0 + cg * 4)), c0 + cg * 4,
+                          f32x4{out[0], out[1], out[2], out[3]});
+    else
+      __builtin_nontemporal_store(f32x4{out[0], out[1], out[2], out[3]}, reinterpret_cast<f32x4*>(y));
   }
 }
 
@@ -676,6 +879,50 @@ extern "C" int64_t prpe_upconv3x3_workspace_bytes(const prpe_view* z, const prpe
   return (int64_t)sizeof(float) * 3 * y->n * z->h * y->w * y->c;
 }
 
+// host restatement of bilin_src (the same float arithmetic) for the DMA kernel's geometry rules
+static void bilin_src_h(int dst, int in, int out, int ac, int& i0, int& i1) {
+  float src;
+  if (ac) {
+    const float scale = out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+    src = scale * (float)dst;
+  } else {
+    const float scale = (float)in / (float)out;
+    src = scale * ((float)dst + 0.5f) - 0.5f;
+    src = src < 0.f ? 0.f : src;
+  }
+  i0 = (int)src;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 < in - 1 ? i0 + 1 : i0;
+}
+
+static bool upd_geometry_ok(const prpe_view* z, const prpe_view* y, int ac) {
+  const int Hi = z->h, Wi = z->w, Ho = y->h, Wo = y->w;
+  if (Hi < 2 || Ho < 5 * Hi) return false;
+  // source window of every 32-column tile (+1 column each side) <= UPD_NSC columns
+  for (int ox0 = 0; ox0 < Wo; ox0 += UPD_W) {
+    int lo, hi, t;
+    bilin_src_h(ox0 > 0 ? ox0 - 1 : 0, Wi, Wo, ac, lo, t);
+    bilin_src_h(ox0 + UPD_W < Wo ? ox0 + UPD_W : Wo - 1, Wi, Wo, ac, t, hi);
+    if (hi - lo + 1 > UPD_NSC) return false;
+  }
+  // every source interval (output rows with the same y0) spans >= 5 output rows, except the first
+  // and the last (the prologue waits for everything; no event follows the last)
+  int prev = -1, run = 0, first = 1;
+  for (int oy = 0; oy < Ho; ++oy) {
+    int y0, y1;
+    bilin_src_h(oy, Hi, Ho, ac, y0, y1);
+    if (y0 != prev) {
+      if (prev >= 0 && !first && run < 5) return false;
+      if (prev >= 0) first = 0;
+      prev = y0;
+      run = 0;
+    }
+    ++run;
+  }
+  const int64_t zb = ((int64_t)(Hi - 1) * z->sh + (int64_t)(Wi - 1) * z->sw + z->c) * 4;
+  return zb < (1LL << 31) && z->sh >= 0 && z->sw >= 0 && y->sh >= 0 && y->sw >= 0;
+}
+
 extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,
                               const float* scale, const float* bias, const float* slope, int32_t act,
                               int32_t y_planes, void* workspace, int64_t workspace_bytes, void* stream) {
@@ -710,6 +957,32 @@ extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t al
       hipLaunchKernelGGL(upconv_out_kernel<1>, g_out, dim3(256), 0, st, p, (const float*)H);
     }
     return launch_status();
+  }
+  // LDS-DMA path (upconv_dma_kernel): 4-channel vectors, Co % 32 == 0, channel-contiguous y,
+  // every output column tile's source window <= UPD_NSC columns, every source interval >= 5
+  // output rows (the kernel's vmcnt counting), one frame of z < 2^31 bytes. PRPE_UPCONV_DMA=0
+  // keeps the fused kernel (A/B runs).
+  static const int dma_env = [] {
+    const char* e = getenv("PRPE_UPCONV_DMA");
+    return e ? atoi(e) : 1;
+  }();
+  if (dma_env && v4 && y->c % UPD_C == 0 && y->sc == 1 && z->sc == 1 && y->h <= UP_MAX_R && upd_geometry_ok(z, y, p.ac)) {
+    const int R = y->h, rblocks = 1;
+    const int ctiles = (y->w + UPD_W - 1) / UPD_W, cblocks = y->c / UPD_C;
+    const int64_t nb = (int64_t)y->n * rblocks * ctiles * cblocks;
+    if (nb < (1LL << 31)) {
+      const dim3 g((unsigned)nb);
+#define PRPE_UPD(A)                                                                                               \
+  if (y_planes) hipLaunchKernelGGL((upconv_dma_kernel<A, true>), g, dim3(256), 0, st, p, R, rblocks, ctiles, cblocks);  \
+  else hipLaunchKernelGGL((upconv_dma_kernel<A, false>), g, dim3(256), 0, st, p, R, rblocks, ctiles, cblocks);
+      if (act == PRPE_ACT_NONE) { PRPE_UPD(PRPE_ACT_NONE) }
+      else if (act == PRPE_ACT_SILU) { PRPE_UPD(PRPE_ACT_SILU) }
+      else if (act == PRPE_ACT_PRELU) { PRPE_UPD(PRPE_ACT_PRELU) }
+      else if (act == PRPE_ACT_GELU) { PRPE_UPD(PRPE_ACT_GELU) }
+      else { PRPE_UPD(-1) }
+#undef PRPE_UPD
+      return launch_status();
+    }
   }
   // fused path: R output rows per thread; shrink R while the grid would not fill the chip
   // rows per thread: each thread's first rows rebuild both interpolation rows of every dy, so

@@ -879,12 +879,13 @@ def test_epilogue_activation_accuracy(act):
                                         (16, 12, 64, 48, False), (7, 9, 20, 13, False), (20, 20, 23, 21, True),
                                         (20, 20, 112, 112, True), (9, 5, 40, 17, False), (13, 6, 37, 11, True),
                                         (20, 7, 51, 9, False), (11, 4, 61, 8, True)])
-def test_upconv_fused_matches_separable(hi, wi, ho, wo, ac):
-    """The one-pass rolling-row kernel and the two-pass separable form evaluate the same sum in
+@pytest.mark.parametrize("Co", [24, 64])
+def test_upconv_fused_matches_separable(hi, wi, ho, wo, ac, Co):
+    """The one-pass kernels (rolling-row; LDS-DMA where Co % 32 == 0 and the ratio is >= 5, i.e.
+    Co = 64 at the adapters' ratios) and the two-pass separable form evaluate the same sum in
     the same rounding sequence (pointwise.hip lerp_add): bit-identical, at the adapters'
     upsampling ratios and at awkward ones (source intervals of 1-2 output rows, both
     align_corners modes)."""
-    Co = 24
     z = rnd(2, hi, wi, 9 * Co, seed=103).to(DEV)
     sc = (torch.rand(Co, generator=_g(104)) + 0.5).to(DEV)
     bi = rnd(Co, seed=105).to(DEV)
@@ -894,6 +895,31 @@ def test_upconv_fused_matches_separable(hi, wi, ho, wo, ac):
         ops.upconv3x3(z, y, ac, sc, bi, None, "gelu", separable=sep)
         outs.append(y.cpu())
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("hi,wi,ho,wo,co,act", [(20, 20, 160, 160, 512, "silu"), (20, 20, 256, 192, 256, "gelu"),
+                                              (20, 20, 112, 112, 256, "prelu"), (20, 20, 100, 70, 96, "none")])
+@pytest.mark.parametrize("planes", [False, True])
+def test_upconv_dma_kernel_model_shapes_bit_exact(hi, wi, ho, wo, co, act, planes):
+    """The LDS-DMA upconv (the adapters' shapes: face-YOLO 20->160 Co 512, ViTPose 20->256x192
+    Co 256, AdaFace 20->112 Co 256, and a ragged column tile) == the separable form bit for bit,
+    fp32 output and planes output (hi = RNE(v), lo = RNE(v - hi) of the same values)."""
+    z = rnd(2, hi, wi, 9 * co, seed=128).to(DEV)
+    sc = (torch.rand(co, generator=_g(129)) + 0.5).to(DEV)
+    bi = rnd(co, seed=130).to(DEV)
+    sl = (torch.rand(co, generator=_g(131)) * 0.3).to(DEV) if act == "prelu" else None
+    ref = torch.empty(2, ho, wo, co, device=DEV)
+    ops.upconv3x3(z, ref, True, sc, bi, sl, act, separable=True)
+    y = torch.empty(2, ho, wo, co, device=DEV)
+    ops.upconv3x3(z, y, True, sc, bi, sl, act, y_planes=planes)
+    torch.cuda.synchronize()
+    if planes:
+        h, l = _decode_planes(y.cpu())
+        v = ref.cpu()
+        assert torch.equal(h, v.to(torch.bfloat16).float())
+        assert torch.equal(l, (v - h).to(torch.bfloat16).float())
+    else:
+        assert torch.equal(y.cpu(), ref.cpu())
 
 
 def test_upconv_nchw_output_view():

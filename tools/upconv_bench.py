@@ -19,7 +19,7 @@ from prpe import ops  # noqa: E402
 # name: (Hi, Wi, Ho, Wo, Co, align_corners, act)
 SHAPES = {
     "yolo_adapter.4 20->160 Co512": (20, 20, 160, 160, 512, True, "silu"),
-    "ada_adapter.4 20->112 Co512": (20, 20, 112, 112, 512, True, "prelu"),
+    "ada_adapter.4 20->112 Co256": (20, 20, 112, 112, 256, True, "prelu"),
     "vit_adapter.4 20->256x192 Co256": (20, 20, 256, 192, 256, True, "gelu"),
     "vit head 16x12->64x48 Co17": (16, 12, 64, 48, 17, False, "none"),
 }
