@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PRPE_ABI_VERSION 5
+#define PRPE_ABI_VERSION 6
 
 /* activations (epilogues/prologues) */
 enum prpe_act {
@@ -148,6 +148,31 @@ typedef struct prpe_conv_desc {
  * prpe_conv2d would reject. Host-only: no launch, no allocation. */
 int64_t prpe_conv2d_workspace_bytes(const prpe_conv_desc* d);
 int prpe_conv2d(const prpe_conv_desc* d, void* stream);
+
+/*
+ * Fused ResNet bottleneck with identity shortcut, precision 3 (torchvision Bottleneck.forward,
+ * v1.5; the reference trunk's layer1 blocks 1-2, modify_models.py:413-446):
+ *   y = relu(bn3(conv3(relu(bn2(conv2_3x3(relu(bn1(conv1(x)))))))) + x)
+ * x, y: [N, H, W, 4*mid] channel-contiguous (x 16-B aligned rows); x_amax [N] per-frame max|x|
+ * (as prpe_conv2d precision 3); y_amax (optional) raised to max|y[n]|. Weights as prpe_conv2d's
+ * precision-3 packs: fp16 planes w_h16 / w_l16 [co_pad][k_pad] (conv1 k = 4 mid, conv2 chunk-major
+ * k = 9 mid, conv3 k = mid), scale16 (the planes' 2^-e folded in) and bias [Co]. The two inner
+ * activations never reach HBM; they are rounded to fp16 planes with one power-of-2 scale per
+ * 8 x 16 output tile (per frame and tile: frames stay independent). mid = 64 (layer1).
+ */
+typedef struct prpe_bneck_desc {
+  prpe_view x;
+  prpe_view y;
+  const float* x_amax;
+  float* y_amax;
+  int32_t mid;
+  const uint16_t* w_h16[3];
+  const uint16_t* w_l16[3];
+  int32_t k_pad[3];
+  const float* scale16[3];
+  const float* bias[3];
+} prpe_bneck_desc;
+int prpe_bottleneck(const prpe_bneck_desc* d, void* stream);
 
 /*
  * conv3x3(pad 1) o bilinear-upsample, second stage of the exact algebraic rewrite

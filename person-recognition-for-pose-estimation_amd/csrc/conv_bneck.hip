@@ -1,0 +1,416 @@
+// Fused ResNet-50 bottleneck with identity shortcut (torchvision Bottleneck.forward, v1.5; the
+// reference's trunk, training/modify_models.py:413-446):
+//   y = relu(bn3(conv3(relu(bn2(conv2_3x3(relu(bn1(conv1(x)))))))) + x)
+// in ONE kernel per 8 x 16 output-pixel tile, precision 3 (two fp16 planes, three MFMA terms).
+//
+// Why: layer1's identity blocks run as three HBM-bound launches (conv1 reads the 256-channel
+// block input, 6.7 GB at bs = 256, writes t1; conv2 reads t1 with its halo and writes t2; conv3
+// reads t2 AND the block input again as the residual and writes y: ~27 GB per block, 7.0 ms,
+// profiles/r03_layer_profile_bufaddr.txt). Here t1 and t2 live only in LDS, the block input is
+// read once (plus the 3x3 halo, mostly L2) and y written once: ~14 GB.
+//
+// Phases of one workgroup (8 waves):
+//   1. t1 = relu(bn1(W1 x)) on the tile's 10 x 18 haloed pixels (12 row blocks of 16), A straight
+//      from global (buffer loads; pixels outside the image read zeros and their t1 is forced to
+//      0 = conv2's zero padding), split into fp16 planes with the frame's scale (x_amax[n], as
+//      the unfused conv1), W1 through an LDS-DMA ring. t1 is then written to LDS as fp16 planes
+//      of t1 * s1 with ONE scale per tile, s1 = 2^(15 - e), max|t1 over the tile| < 2^e (a
+//      block-wide max): t1's operand rounding depends only on this tile of this frame, so frames
+//      stay independent of their batch-mates.
+//   2. t2 = relu(bn2(conv2(t1))): conv_halo.hip's K-loop (9 taps x 2 chunks) on the LDS tile,
+//      planes read without a split; t2 -> LDS as fp16 planes with the tile's scale s2.
+//   3. y = relu(bn3(W3 t2) + x): W3 in two 128-column halves through LDS, residual read from
+//      global, y written from the MFMA accumulator layout, per-frame max|y| raised (y_amax).
+// Epilogue arithmetic as conv_wave.hip (scale16 carries the weights' 2^-e, the activation
+// scale is removed exactly); only t1 / t2 are rounded with per-tile instead of per-frame
+// scales, so results agree with the unfused launches to the precision-3 operand error
+// (tests/test_gpu_ops.py: vs fp64 and vs the unfused path).
+//
+// LDS (64 KB, two workgroups per CU): TT [2 chunks][192 px][128 B] (t1, then t2 in its first
+// 32 KB), the swizzled planes layout of conv_halo.hip (slot s of pixel q at s ^ ((q >> 1) & 7));
+// the W1 / W2 ring [2][2 planes][64 rows][64 B] right after it; phase 3's W3 half
+// [2 K-steps][2 planes][128 rows][64 B] overlays TT's last 16 KB and the ring.
+#include "conv.h"
+
+namespace prpe_k {
+
+struct BneckK {
+  const float* x; int64_t xsn, xsh, xsw; const float* x_amax;
+  float* y; int64_t ysn, ysh, ysw; float* y_amax;
+  int N, H, W;
+  const uint16_t* wh[3]; const uint16_t* wl[3];
+  int kp[3];
+  const float* sc[3]; const float* bi[3];
+  int tiles_w, tiles_h, nwg;
+};
+
+namespace {
+
+constexpr int BK_ = 32;
+constexpr int MID = 64, CIO = 256, TR = 8, TC = 16, NW = 8;
+constexpr int HW_ = TC + 2, HP = (TR + 2) * HW_;        // 18, 180 haloed pixels
+constexpr int NRB1 = (HP + 15) / 16;                     // 12 row blocks of haloed pixels
+constexpr int CHB1 = NRB1 * 16 * 128;                    // bytes of one 32-channel chunk of t1
+constexpr int CHB2 = TR * TC * 128;                      // ... of t2
+constexpr int TT_BYTES = (MID / 32) * CHB1;              // 48 KB
+constexpr int STAGE = 2 * MID * 64;                      // one K-step of W1 / W2 (both planes)
+constexpr int RING_OFF = TT_BYTES;
+constexpr int W3_OFF = (MID / 32) * CHB2;                // 32 KB: after t2
+constexpr int W3_STEP = 2 * 128 * 64;                    // one K-step of a W3 half (both planes)
+constexpr int LDS_BYTES = TT_BYTES + 2 * STAGE;          // 64 KB
+static_assert(W3_OFF + (MID / 32) * W3_STEP <= LDS_BYTES, "W3 half overlay");
+
+__device__ __forceinline__ unsigned fbits(float v) { return __builtin_bit_cast(unsigned, v); }
+
+// write the fp16 planes of a (>= 0, scaled) value into the planes layout: pixel q, channel c
+__device__ __forceinline__ void put_planes(unsigned char* base, int chb, int q, int c, uint16_t hi, uint16_t lo) {
+  const int sw = (q >> 1) & 7, g = (c & 31) >> 3, e = c & 7;
+  unsigned char* pq = base + (c >> 5) * chb + q * 128;
+  *reinterpret_cast<uint16_t*>(pq + (((2 * g) ^ sw) << 4) + e * 2) = hi;
+  *reinterpret_cast<uint16_t*>(pq + (((2 * g + 1) ^ sw) << 4) + e * 2) = lo;
+}
+
+// v >= 0 (post-ReLU) scaled by s -> (hi, lo) fp16 planes, round toward zero (split_planes_f16)
+__device__ __forceinline__ void f16_pair(float v, float s, uint16_t& hi, uint16_t& lo) {
+  const float a = v * s;
+  const auto h = __builtin_amdgcn_cvt_pkrtz(a, 0.f);
+  const float r = a - (float)h[0];
+  const auto l = __builtin_amdgcn_cvt_pkrtz(r, 0.f);
+  hi = __builtin_bit_cast(uint16_t, h[0]);
+  lo = __builtin_bit_cast(uint16_t, l[0]);
+}
+
+// B fragments of column block j from a [2 planes][rows][64 B] stage (conv_wave's slot swizzle)
+__device__ __forceinline__ void b_frags(const unsigned char* sb, int rows, int j, int fr, int fg, f16x8 (&b)[2]) {
+  const int nrow = j * 16 + fr;
+  const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
+  b[0] = *reinterpret_cast<const f16x8*>(bp);
+  b[1] = *reinterpret_cast<const f16x8*>(bp + rows * 64);
+}
+
+// the three partial products of the split, smallest first (conv_wave.hip's order)
+__device__ __forceinline__ f32x4 mfma3(const f16x8 (&a)[2], const f16x8 (&b)[2], f32x4 c) {
+  c = mfma16(a[1], b[0], c);
+  c = mfma16(a[0], b[1], c);
+  c = mfma16(a[0], b[0], c);
+  return c;
+}
+
+__global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
+  __shared__ unsigned tmax[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  int L = xcd_remap(blockIdx.x, p.nwg);
+  const int tw = L % p.tiles_w;
+  L /= p.tiles_w;
+  const int th = L % p.tiles_h;
+  const int n = L / p.tiles_h;
+  const int oh0 = th * TR, ow0 = tw * TC;
+  if (tid < 2) tmax[tid] = 0u;
+
+  // ---- descriptors: this frame of x (phase 1 A and the residual), the six weight planes
+  const float* xn = p.x + (int64_t)n * p.xsn;
+  const int frame_bytes = (int)(((int64_t)(p.H - 1) * p.xsh + (int64_t)(p.W - 1) * p.xsw + CIO) * 4);
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(xn, frame_bytes);
+  __amdgpu_buffer_rsrc_t wr[3][2];
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const int rows = l == 2 ? CIO : MID;
+    wr[l][0] = buf_rsrc(p.wh[l], rows * p.kp[l] * 2);
+    wr[l][1] = buf_rsrc(p.wl[l], rows * p.kp[l] * 2);
+  }
+  // W1 / W2 ring piece of this wave: plane wave / 4, rows 16 (wave % 4) .. +16
+  const int bq = wave >> 2, brb = wave & 3;
+  const int bnrow = brb * 16 + (lane >> 2);
+  const int bch = (lane & 3) ^ swzF(bnrow);
+  const int bdst = RING_OFF + (bq * MID + brb * 16) * 64;
+  auto issue_w = [&](int l, int kt, int stage) {           // l = 0 (W1) or 1 (W2)
+    const unsigned vo = (unsigned)((bnrow * p.kp[l] + bch * 8) * 2);
+    bl_lds16(bq ? wr[l][1] : wr[l][0], lds + bdst + stage * STAGE, vo, kt * BK_ * 2);
+  };
+
+  // =========================== phase 1: t1 on the haloed tile
+  const float am = p.x_amax[n];
+  const int ex = f16_scale_exp(am);
+  const float sa = ldexpf(1.f, 15 - ex), inv0 = ldexpf(1.f, ex - 15);
+  // row blocks wave and wave + 8 (the latter only for waves 0..3)
+  const bool two = wave + NW < NRB1;                         // wave-uniform
+  unsigned av[2];
+  bool pval[2][4];                                           // C-layout rows fg*4 + r: pixel valid
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rb = wave + i * NW;
+    const int px = rb * 16 + fr;
+    const int hr = px / HW_, hc = px - hr * HW_;
+    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+    const bool ok = px < HP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && rb < NRB1;
+    av[i] = ok ? (unsigned)(((int64_t)ih * p.xsh + (int64_t)iw * p.xsw + fg * 8) * 4) : BL_OOB;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int q = rb * 16 + fg * 4 + r;
+      const int qr = q / HW_, qc = q - qr * HW_;
+      pval[i][r] = q < HP && (unsigned)(oh0 - 1 + qr) < (unsigned)p.H && (unsigned)(ow0 - 1 + qc) < (unsigned)p.W;
+    }
+  }
+  f32x4 acc1[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f4 raw[2][2];
+  auto load_a = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if (i == 1 && !two) continue;
+      raw[i][0] = bl_f4(xr, av[i], kt * BK_ * 4);
+      raw[i][1] = bl_f4(xr, av[i] + 16, kt * BK_ * 4);
+    }
+  };
+  f16x8 af[2][2];
+  auto split = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      unsigned long long p0[2], p1[2];
+      split_planes_f16(raw[i][0], sa, p0);
+      split_planes_f16(raw[i][1], sa, p1);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        af[i][q] = __builtin_bit_cast(f16x8, u64x2{p0[q], p1[q]});
+      }
+    }
+  };
+  constexpr int NK1 = CIO / BK_;
+  load_a(0);
+  issue_w(0, 0, 0);
+  split();
+  for (int kt = 0; kt < NK1; ++kt) {
+    wait_barrier<0>();
+    if (kt + 1 < NK1) {
+      load_a(kt + 1);
+      issue_w(0, kt + 1, (kt + 1) & 1);
+    } else {
+      issue_w(1, 0, (kt + 1) & 1);                           // W2's first K-step (phase 2)
+    }
+    const unsigned char* sb = lds + RING_OFF + (kt & 1) * STAGE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f16x8 b[2];
+      b_frags(sb, MID, j, fr, fg, b);
+      acc1[0][j] = mfma3(af[0], b, acc1[0][j]);
+      if (two) acc1[1][j] = mfma3(af[1], b, acc1[1][j]);
+    }
+    if (kt + 1 < NK1) split();
+  }
+  // epilogue 1: bn1 + ReLU (zero outside the image: conv2's padding), tile max, planes -> TT
+  float m1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 16 + fr;
+    const float s = p.sc[0][c], b = p.bi[0][c];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v = fmaf(acc1[i][j][r] * inv0, s, b);
+        v = v > 0.f && pval[i][r] && (i == 0 || two) ? v : 0.f;
+        acc1[i][j][r] = v;
+        m1 = fmaxf(m1, v);
+      }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m1 = fmaxf(m1, __shfl_xor(m1, o, 64));
+  wait_barrier<0>();                                         // every wave's phase-1 reads of the ring done
+  if (lane == 0) atomicMax(&tmax[0], fbits(m1));
+  __syncthreads();
+  const int e1 = f16_scale_exp(__builtin_bit_cast(float, tmax[0]));
+  const float s1 = ldexpf(1.f, 15 - e1), inv1 = ldexpf(1.f, e1 - 15);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (i == 1 && !two) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        uint16_t hi, lo;
+        f16_pair(acc1[i][j][r], s1, hi, lo);
+        put_planes(lds, CHB1, (wave + i * NW) * 16 + fg * 4 + r, j * 16 + fr, hi, lo);
+      }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // t1 in LDS before the next barrier
+
+  // =========================== phase 2: t2 = conv2(t1), the halo K-loop on the LDS tile
+  int aoff[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int px = (wave + t / 3) * HW_ + fr + t % 3;
+    aoff[t] = px * 128 + (((2 * fg) ^ ((px >> 1) & 7)) << 4);
+  }
+  f32x4 acc2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  constexpr int NK2 = (MID / 32) * 9;
+  int kt2 = 0;
+#pragma unroll 1
+  for (int c = 0; c < MID / 32; ++c) {
+    const unsigned char* tc = lds + c * CHB1;
+#pragma unroll
+    for (int t = 0; t < 9; ++t, ++kt2) {
+      // K-step k of W2 sits in ring stage k & 1 (its step 0 was issued by phase 1's last step)
+      wait_barrier<0>();
+      if (kt2 + 1 < NK2) issue_w(1, kt2 + 1, (kt2 + 1) & 1);
+      f16x8 a[2];
+      a[0] = *reinterpret_cast<const f16x8*>(tc + aoff[t]);
+      a[1] = *reinterpret_cast<const f16x8*>(tc + (aoff[t] ^ 16));
+      const unsigned char* sb = lds + RING_OFF + (kt2 & 1) * STAGE;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f16x8 b[2];
+        b_frags(sb, MID, j, fr, fg, b);
+        acc2[j] = mfma3(a, b, acc2[j]);
+      }
+    }
+  }
+  // epilogue 2: bn2 + ReLU, tile max, planes -> TT (t1 is dead once every wave is past here)
+  const int oy = oh0 + wave;
+  float m2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = j * 16 + fr;
+    const float s = p.sc[1][c], b = p.bi[1][c];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = fmaf(acc2[j][r] * inv1, s, b);
+      v = v > 0.f && oy < p.H && ow0 + fg * 4 + r < p.W ? v : 0.f;
+      acc2[j][r] = v;
+      m2 = fmaxf(m2, v);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m2 = fmaxf(m2, __shfl_xor(m2, o, 64));
+  wait_barrier<0>();                                         // all t1 / W2 reads done, TT and ring free
+  if (lane == 0) atomicMax(&tmax[1], fbits(m2));
+  // W3 half 0 into the overlay (TT's last 16 KB + the ring): 32 pieces, 4 per wave
+  auto issue_w3 = [&](int h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = wave * 4 + i;
+      const int ks = idx >> 4, q = (idx >> 3) & 1, rb = idx & 7;
+      const int nrow = rb * 16 + (lane >> 2);
+      const int ch = (lane & 3) ^ swzF(nrow);
+      const unsigned vo = (unsigned)(((h * 128 + nrow) * p.kp[2] + ch * 8) * 2);
+      bl_lds16(q ? wr[2][1] : wr[2][0], lds + W3_OFF + ks * W3_STEP + (q * 128 + rb * 16) * 64, vo, ks * BK_ * 2);
+    }
+  };
+  issue_w3(0);
+  __syncthreads();
+  const int e2 = f16_scale_exp(__builtin_bit_cast(float, tmax[1]));
+  const float s2 = ldexpf(1.f, 15 - e2), inv2 = ldexpf(1.f, e2 - 15);
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      uint16_t hi, lo;
+      f16_pair(acc2[j][r], s2, hi, lo);
+      put_planes(lds, CHB2, wave * 16 + fg * 4 + r, j * 16 + fr, hi, lo);
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // t2 in LDS before the next barrier
+
+  // =========================== phase 3: y = relu(bn3(W3 t2) + x), two halves of 128 columns
+  const int q3 = wave * 16 + fr;
+  const int a3 = q3 * 128 + (((2 * fg) ^ ((q3 >> 1) & 7)) << 4);
+  float ymax = 0.f;
+#pragma unroll 1
+  for (int h = 0; h < 2; ++h) {
+    if (h == 0) {
+      wait_barrier<0>();                                     // W3 half 0 landed, t2 written
+    } else if (oy < p.H) {
+      // W3 half 1 was issued before half 0's residual loads and stores (<= 64 younger ops):
+      // leaving the 32 youngest in flight still covers it; then publish every wave's pieces
+      asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
+    } else {
+      wait_barrier<0>();                                     // a wave with no valid row issued nothing after it
+    }
+    f32x4 acc3[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc3[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < MID / 32; ++ks) {
+      f16x8 a[2];
+      a[0] = *reinterpret_cast<const f16x8*>(lds + ks * CHB2 + a3);
+      a[1] = *reinterpret_cast<const f16x8*>(lds + ks * CHB2 + (a3 ^ 16));
+      const unsigned char* sb = lds + W3_OFF + ks * W3_STEP;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        f16x8 b[2];
+        b_frags(sb, 128, j, fr, fg, b);
+        acc3[j] = mfma3(a, b, acc3[j]);
+      }
+    }
+    if (h == 0) {
+      // every wave is done reading W3 half 0 (its ds_reads fed the MFMAs above): overwrite it
+      // with half 1 now, BEFORE this half's residual loads and stores
+      asm volatile("s_barrier" ::: "memory");
+      issue_w3(1);
+      asm volatile("" ::: "memory");
+    }
+    // residual + bn3 + ReLU, stored from the accumulator layout (16 channels = 64 B per row)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = h * 128 + j * 16 + fr;
+      const float s = p.sc[2][c], b = p.bi[2][c];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ox = ow0 + fg * 4 + r;
+        if (oy >= p.H || ox >= p.W) continue;
+        const float res = xn[(int64_t)oy * p.xsh + (int64_t)ox * p.xsw + c];
+        float v = fmaf(acc3[j][r] * inv2, s, b) + res;
+        v = v > 0.f ? v : 0.f;
+        p.y[(int64_t)n * p.ysn + (int64_t)oy * p.ysh + (int64_t)ox * p.ysw + c] = v;
+        ymax = fmaxf(ymax, v);
+      }
+    }
+  }
+  if (p.y_amax) amax_commit(p.y_amax + n, ymax);
+}
+
+}  // namespace
+
+int bneck_launch(const BneckK& kp0, hipStream_t st) {
+  BneckK kp = kp0;
+  kp.tiles_w = (kp.W + TC - 1) / TC;
+  kp.tiles_h = (kp.H + TR - 1) / TR;
+  const int64_t nwg = (int64_t)kp.N * kp.tiles_w * kp.tiles_h;
+  if (nwg <= 0 || nwg >= (1LL << 31)) return PRPE_EINVAL;
+  kp.nwg = (int)nwg;
+  hipLaunchKernelGGL(bneck_kernel, dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  return launch_status();
+}
+
+}  // namespace prpe_k
+
+extern "C" int prpe_bottleneck(const prpe_bneck_desc* d, void* stream) {
+  using namespace prpe_k;
+  if (!d || !view_ok(&d->x) || !view_ok(&d->y) || !d->x_amax) return PRPE_EINVAL;
+  const prpe_view& x = d->x; const prpe_view& y = d->y;
+  if (d->mid != MID || x.c != CIO || y.c != CIO || x.n != y.n || x.h != y.h || x.w != y.w) return PRPE_EINVAL;
+  if (x.sc != 1 || y.sc != 1 || x.sw % 4 || x.sh % 4 || x.sn % 4 || (uintptr_t)x.ptr % 16 || x.sw < 0 || x.sh < 0 ||
+      y.sw < 0 || y.sh < 0)
+    return PRPE_EINVAL;
+  const int kneed[3] = {CIO, 9 * MID, MID};
+  for (int l = 0; l < 3; ++l) {
+    if (!d->w_h16[l] || !d->w_l16[l] || !d->scale16[l] || !d->bias[l] || d->k_pad[l] != kneed[l]) return PRPE_EINVAL;
+    if ((uintptr_t)d->w_h16[l] % 16 || (uintptr_t)d->w_l16[l] % 16) return PRPE_EINVAL;
+  }
+  if (((int64_t)(x.h - 1) * x.sh + (int64_t)(x.w - 1) * x.sw + CIO) * 4 >= (1LL << 31)) return PRPE_EINVAL;
+  BneckK kp{};
+  kp.x = x.ptr; kp.xsn = x.sn; kp.xsh = x.sh; kp.xsw = x.sw; kp.x_amax = d->x_amax;
+  kp.y = y.ptr; kp.ysn = y.sn; kp.ysh = y.sh; kp.ysw = y.sw; kp.y_amax = d->y_amax;
+  kp.N = x.n; kp.H = x.h; kp.W = x.w;
+  for (int l = 0; l < 3; ++l) {
+    kp.wh[l] = d->w_h16[l]; kp.wl[l] = d->w_l16[l]; kp.kp[l] = d->k_pad[l];
+    kp.sc[l] = d->scale16[l]; kp.bi[l] = d->bias[l];
+  }
+  return bneck_launch(kp, as_stream(stream));
+}

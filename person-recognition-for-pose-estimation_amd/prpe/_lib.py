@@ -14,7 +14,7 @@ from ._srchash import source_hash
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libprpe.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class PrpeError(RuntimeError):
@@ -44,6 +44,12 @@ class ConvDesc(C.Structure):
                 ("n2", C.c_int32), ("workspace", C.c_void_p), ("workspace_bytes", C.c_int64)]
 
 
+class BneckDesc(C.Structure):
+    _fields_ = [("x", View), ("y", View), ("x_amax", C.c_void_p), ("y_amax", C.c_void_p), ("mid", C.c_int32),
+                ("w_h16", C.c_void_p * 3), ("w_l16", C.c_void_p * 3), ("k_pad", C.c_int32 * 3),
+                ("scale16", C.c_void_p * 3), ("bias", C.c_void_p * 3)]
+
+
 ACT = {"none": 0, "relu": 1, "silu": 2, "prelu": 3, "gelu": 4, "sigmoid": 5}
 RES_NONE, RES_PRE, RES_POST = 0, 1, 2
 
@@ -56,6 +62,7 @@ _VP = C.POINTER(View)
 SIGNATURES = {
     "prpe_conv2d_workspace_bytes": (C.c_int64, [C.POINTER(ConvDesc)]),
     "prpe_conv2d": (C.c_int, [C.POINTER(ConvDesc), _P]),
+    "prpe_bottleneck": (C.c_int, [C.POINTER(BneckDesc), _P]),
     "prpe_upconv3x3_workspace_bytes": (C.c_int64, [_VP, _VP]),
     "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _I, _P, _L, _P]),
     "prpe_dwconv": (C.c_int, [_VP, _VP, _VP, _P, _I, _I, _I, _P, _P, _I, _P]),

@@ -49,6 +49,9 @@ SMALLCO_TAPS = os.environ.get("PRPE_SMALLCO_TAPS", "1") != "0"
 # .10), the tap GEMM runs in the producer's epilogue (prpe_conv_desc.w2): the 128-channel map
 # never reaches HBM. PRPE_TAPS_FUSE=0 runs the two convs separately.
 TAPS_FUSE = os.environ.get("PRPE_TAPS_FUSE", "1") != "0"
+# ResNet-50 layer1 identity blocks (1.1, 1.2) as ONE fused launch each (prpe_bottleneck: t1 / t2
+# only in LDS). PRPE_BNECK_FUSE=0 runs the three convs separately.
+BNECK_FUSE = os.environ.get("PRPE_BNECK_FUSE", "1") != "0"
 
 
 class _Prec:
@@ -90,6 +93,7 @@ class Engine:
         # tensors, cursor (chunk index, offset)]
         self._amax_pools: dict[str, list] = {}
         self._amax_scope = None
+        self._amax_epoch: dict[str, int] = {}   # comp -> number of times its pool was zeroed
 
     def prec(self, comp):
         return _Prec(self, comp)
@@ -140,6 +144,7 @@ class Engine:
             t.zero_()
         pool[1] = pool[2] = 0
         self._amax_scope = comp
+        self._amax_epoch[comp] = self._amax_epoch.get(comp, 0) + 1
 
     def amax_slot(self, n: int):
         """[n] zeroed slots from the current precision-3 component's pool."""
@@ -185,17 +190,18 @@ class Engine:
         return p
 
     def conv(self, x, p: ConvPack, out=None, res=None, res_mode=0, act=None, x2=None, x2_amax=None,
-             planes_out=False, w2=None, y2=None, **stage2):
+             planes_out=False, w2=None, y2=None, prec=None, **stage2):
         """``x2``: second 1x1 input on the output grid (dual-input GEMM, see prpe.h).
         ``planes_out``: the only consumer is a precision-0 wave-row conv: write the planes format.
         ``w2``/``y2``: epilogue 1x1 GEMM into y2 (prpe.h); ``out`` is then not written;
-        ``stage2``: its second stage (w3, scale2, bias2, act2; prpe.h)."""
+        ``stage2``: its second stage (w3, scale2, bias2, act2; prpe.h).
+        ``prec``: this conv's precision instead of the component's (Engine.feat_prec)."""
         B, H, W, _ = x.shape
         Ho = (H + 2 * p.pad - p.kh) // p.stride + 1
         Wo = (W + 2 * p.pad - p.kw) // p.stride + 1
         if out is None:
             out = self.empty(B, Ho, Wo, p.co)
-        prec = self.precision
+        prec = self.precision if prec is None else prec
         if prec == 3 and (not self._f16_ok(x, p, out, res) or (x2 is not None and x2_amax is None)):
             prec = 2
         xa = getattr(x, "_prpe_amax", None) if prec == 3 else None
@@ -268,7 +274,21 @@ class Engine:
         """MultiTaskResNetFeatureExtractor (modify_models.py:427-437), torchvision v1.5.
         ``flip_w``: run on the W-mirrored frames (torch.flip(images, dims=[-1]))."""
         with self.prec("trunk"):
-            return self._trunk(x_nchw, flip_w)
+            y = self._trunk(x_nchw, flip_w)
+            y._prpe_amax_tag = ("trunk", self._amax_epoch.get("trunk"))
+            return y
+
+    def feat_prec(self, feat):
+        """Precision of a head's first conv over the trunk output ``feat``: 3 (fp32-faithful at
+        the 3-term cost) while ``feat``'s per-frame max|x| slots are still the ones its trunk
+        call wrote (the trunk pool is re-zeroed by the next trunk call), else the head's own.
+        Measured: the face-YOLO adapter's 2048-deep .0 GEMM at precision 0 carried most of the
+        box-coordinate error of policy "auto" (tools/yolo_adapter_prec_diag.py)."""
+        tag = getattr(feat, "_prpe_amax_tag", None)
+        if tag is not None and getattr(feat, "_prpe_amax", None) is not None and \
+                self._amax_epoch.get(tag[0]) == tag[1] and self.policy.get("trunk") == 3:
+            return 3
+        return None
 
     def stem(self, x_nchw, flip_w=False):
         """conv1 7x7/2 pad 3 + bn1 + relu (torchvision resnet50) as a channel-chunked conv.
@@ -288,7 +308,7 @@ class Engine:
                 del self._aux[k]                       # one batch shape at a time
             buf = torch.zeros(B0, H0 + 6, W0 + 8, 4, device=self.device, dtype=torch.float32)
             self._aux[key] = buf
-        amax = self.amax_slot(B0)
+        amax = self.amax_slot(B0) if self.precision == 3 else None
         ops.copy_pad(ops.nhwc(x_nchw), buf[:, 3:3 + H0, 3:3 + W0, :], flip_w=flip_w, y_amax=amax)
         v = buf.as_strided((B0, H0 + 6, W0, 32), (buf.stride(0), buf.stride(1), 4, 1))
         v._prpe_amax = amax
@@ -313,6 +333,9 @@ class Engine:
             for b in range(blocks):
                 q = f"backbone.layer{li}.{b}"
                 s = stride if b == 0 else 1
+                if b > 0 and self._bneck_ok(x, planes):
+                    x = self.bottleneck(q, x)
+                    continue
                 o = self.conv(x, self.pk(q + ".conv1", q + ".conv1.weight", bn=q + ".bn1", act="relu"))
                 o = self.conv(o, self.pk(q + ".conv2", q + ".conv2.weight", s, 1, bn=q + ".bn2", act="relu"))
                 if b == 0:
@@ -324,6 +347,30 @@ class Engine:
                     x = self.conv(o, self.pk(q + ".conv3", q + ".conv3.weight", bn=q + ".bn3", act="relu"),
                                   res=x, res_mode=RES_PRE)
         return x
+
+    def _bneck_ok(self, x, planes):
+        return (BNECK_FUSE and self.precision == 3 and planes == 64 and x.shape[3] == 4 * planes and
+                x.is_contiguous() and getattr(x, "_prpe_amax", None) is not None)
+
+    def bottleneck(self, q, x):
+        """Identity-shortcut bottleneck ``q`` (torchvision Bottleneck.forward) as one fused launch
+        (prpe_bottleneck); same packs as the unfused path."""
+        packs = (self.pk(q + ".conv1", q + ".conv1.weight", bn=q + ".bn1", act="relu"),
+                 self.pk(q + ".conv2", q + ".conv2.weight", 1, 1, bn=q + ".bn2", act="relu"),
+                 self.pk(q + ".conv3", q + ".conv3.weight", bn=q + ".bn3", act="relu"))
+        y = self.empty(*x.shape)
+        ya = self.amax_slot(x.shape[0])
+        if q in self.watch:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ops.bottleneck(x, packs, y, x._prpe_amax, ya)
+            e1.record()
+            self.events.setdefault(q, []).append((e0, e1, x.shape[0] * x.shape[1] * x.shape[2], packs[1], 3,
+                                                  x.numel()))
+        else:
+            ops.bottleneck(x, packs, y, x._prpe_amax, ya)
+        y._prpe_amax = ya
+        return y
 
     # ------------------------------------------------------------------ YOLO v11n branch
     def yc(self, q, x, k, s=1, act="silu", out=None, res=None, res_mode=0):
@@ -412,7 +459,8 @@ class Engine:
 
     def yolo_adapter(self, p, feat):
         a = p + ".adapter"
-        t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="silu"))
+        t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="silu"),
+                      prec=self.feat_prec(feat))
         u = self.upconv(a + ".4", t, a + ".4.weight", (160, 160), True, bn=a + ".5", bias_key=a + ".4.bias",
                         act="silu", planes=True)
         t = self.conv(u, self.pk(a + ".7", a + ".7.weight", bn=a + ".8", bias_key=a + ".7.bias", act="silu"),
@@ -505,7 +553,7 @@ class Engine:
     def _adaface(self, feat):
         a = "ada_face.adapter"
         t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="prelu",
-                                    prelu=a + ".2.weight"))
+                                    prelu=a + ".2.weight"), prec=self.feat_prec(feat))
         u = self.upconv(a + ".4", t, a + ".4.weight", (112, 112), True, bn=a + ".5", bias_key=a + ".4.bias",
                         act="prelu", prelu=a + ".6.weight", planes=True)
         t = self.conv(u, self.pk(a + ".7", a + ".7.weight", 1, 1, bn=a + ".8", bias_key=a + ".7.bias", act="prelu",
@@ -553,7 +601,8 @@ class Engine:
     def vit_adapter(self, feat):
         """CustomVitPose.adapter (modify_models.py:352-374) -> pixel_values NHWC [B,256,192,3]."""
         a = "vit_pose.adapter"
-        t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="gelu"))
+        t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="gelu"),
+                      prec=self.feat_prec(feat))
         u = self.upconv(a + ".4", t, a + ".4.weight", arch.VIT_IMG, True, bn=a + ".5", bias_key=a + ".4.bias",
                         act="gelu", planes=True)
         p7 = self.pk(a + ".7", a + ".7.weight", 1, 1, bn=a + ".8", bias_key=a + ".7.bias", act="gelu")

@@ -10,7 +10,7 @@ import ctypes as C
 
 import torch
 
-from ._lib import ACT, RES_NONE, ConvDesc, PrpeError, View, check, lib
+from ._lib import ACT, RES_NONE, BneckDesc, ConvDesc, PrpeError, View, check, lib
 
 
 def _stream() -> C.c_void_p:
@@ -105,6 +105,26 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
         ws = torch.empty((nbytes + 255) // 256 * 64, device=y.device, dtype=torch.float32)
         d.workspace, d.workspace_bytes = ws.data_ptr(), nbytes
     check(lib().prpe_conv2d(C.byref(d), _stream()), f"prpe_conv2d[{pack.name}]")
+    return y
+
+
+def bottleneck(x, packs, y, x_amax, y_amax=None):
+    """Fused identity-shortcut ResNet bottleneck at precision 3 (prpe_bottleneck, include/prpe.h):
+    y = relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1 x))))))) + x); ``packs`` = the three
+    ConvPacks (BN folded, conv2 chunk-major), x_amax [N] per-frame max|x|, y_amax [N] raised."""
+    _gpu(x, y, x_amax)
+    d = BneckDesc()
+    d.x, d.y = view(x), view(y)
+    d.x_amax, d.y_amax = x_amax.data_ptr(), _ptr(y_amax)
+    d.mid = packs[0].co
+    keep = []
+    for i, pk in enumerate(packs):
+        h16, l16, s16 = pk.f16_planes()
+        b = pk.bias if pk.bias is not None else torch.zeros(pk.co, device=x.device)
+        keep.append(b)
+        d.w_h16[i], d.w_l16[i], d.scale16[i], d.bias[i] = h16.data_ptr(), l16.data_ptr(), s16.data_ptr(), b.data_ptr()
+        d.k_pad[i] = pk.k_pad
+    check(lib().prpe_bottleneck(C.byref(d), _stream()), "prpe_bottleneck")
     return y
 
 

@@ -30,6 +30,9 @@ def main():
     m.forward_all(x, face_stride=[8.0, 16.0, 32.0], concurrent=False)
     torch.cuda.synchronize()
     e.watch = set(e._packs.keys())
+    # fused bottlenecks (Engine.bottleneck) are timed under the block name; their row shows conv2
+    e.watch |= {f"backbone.layer{li}.{b}" for li, (_, n, _) in enumerate(arch.RESNET50_STAGES, 1)
+                for b in range(n)}
     e.events = {}
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
