@@ -159,6 +159,8 @@ int prpe_conv2d(const prpe_conv_desc* d, void* stream);
  * k = 9 mid, conv3 k = mid), scale16 (the planes' 2^-e folded in) and bias [Co]. The two inner
  * activations never reach HBM; they are rounded to fp16 planes with one power-of-2 scale per
  * 8 x 16 output tile (per frame and tile: frames stay independent). mid = 64 (layer1).
+ * x, y, the weight planes, scale16 and bias 16-B aligned, x / y pixel strides multiples of 4
+ * floats, one frame of x and of y < 2^31 bytes; anything else returns -EINVAL.
  */
 typedef struct prpe_bneck_desc {
   prpe_view x;

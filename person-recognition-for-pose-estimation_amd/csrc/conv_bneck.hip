@@ -21,15 +21,19 @@
 //      planes read without a split; t2 -> LDS as fp16 planes with the tile's scale s2.
 //   3. y = relu(bn3(W3 t2) + x): W3 in two 128-column halves through LDS, residual read from
 //      global, y written from the MFMA accumulator layout, per-frame max|y| raised (y_amax).
+// Every MFMA is issued transposed (weights as the A operand, pixels as B), so a lane's
+// accumulator holds 4 consecutive channels of one pixel: the epilogues write t1 / t2 planes with
+// two 8-B LDS stores per 4 channels and read the residual / store y as 16-B buffer accesses.
 // Epilogue arithmetic as conv_wave.hip (scale16 carries the weights' 2^-e, the activation
 // scale is removed exactly); only t1 / t2 are rounded with per-tile instead of per-frame
 // scales, so results agree with the unfused launches to the precision-3 operand error
 // (tests/test_gpu_ops.py: vs fp64 and vs the unfused path).
 //
-// LDS (64 KB, two workgroups per CU): TT [2 chunks][192 px][128 B] (t1, then t2 in its first
+// LDS (80 KB, two workgroups per CU): TT [2 chunks][192 px][128 B] (t1, then t2 in its first
 // 32 KB), the swizzled planes layout of conv_halo.hip (slot s of pixel q at s ^ ((q >> 1) & 7));
-// the W1 / W2 ring [2][2 planes][64 rows][64 B] right after it; phase 3's W3 half
-// [2 K-steps][2 planes][128 rows][64 B] overlays TT's last 16 KB and the ring.
+// the W1 / W2 ring [4 stages][2 planes][64 rows][64 B] right after it (three K-steps of
+// lookahead; the block A operand of phase 1 is loaded two K-steps ahead into registers); phase
+// 3's W3 half [2 K-steps][2 planes][128 rows][64 B] overlays TT's last 16 KB and ring stages 0-1.
 #include "conv.h"
 
 namespace prpe_k {
@@ -57,27 +61,24 @@ constexpr int STAGE = 2 * MID * 64;                      // one K-step of W1 / W
 constexpr int RING_OFF = TT_BYTES;
 constexpr int W3_OFF = (MID / 32) * CHB2;                // 32 KB: after t2
 constexpr int W3_STEP = 2 * 128 * 64;                    // one K-step of a W3 half (both planes)
-constexpr int LDS_BYTES = TT_BYTES + 2 * STAGE;          // 64 KB
-static_assert(W3_OFF + (MID / 32) * W3_STEP <= LDS_BYTES, "W3 half overlay");
+constexpr int RING = 4;                                  // W1 / W2 ring stages (3 K-steps of lookahead)
+constexpr int LDS_BYTES = TT_BYTES + RING * STAGE;       // 80 KB: two workgroups per CU
+static_assert(W3_OFF + (MID / 32) * W3_STEP <= RING_OFF + 2 * STAGE, "W3 half overlay below ring stage 2");
 
-__device__ __forceinline__ unsigned fbits(float v) { return __builtin_bit_cast(unsigned, v); }
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
-// write the fp16 planes of a (>= 0, scaled) value into the planes layout: pixel q, channel c
-__device__ __forceinline__ void put_planes(unsigned char* base, int chb, int q, int c, uint16_t hi, uint16_t lo) {
-  const int sw = (q >> 1) & 7, g = (c & 31) >> 3, e = c & 7;
-  unsigned char* pq = base + (c >> 5) * chb + q * 128;
-  *reinterpret_cast<uint16_t*>(pq + (((2 * g) ^ sw) << 4) + e * 2) = hi;
-  *reinterpret_cast<uint16_t*>(pq + (((2 * g + 1) ^ sw) << 4) + e * 2) = lo;
+// the fp16 planes (4 x f16 each) of channels c0..c0+3 (c0 % 4 == 0, one 8-channel group) of
+// pixel q into the planes layout: two 8-B LDS writes
+__device__ __forceinline__ void put_planes4(unsigned char* base, int chb, int q, int c0, unsigned long long (&pl)[2]) {
+  const int sw = (q >> 1) & 7, g = (c0 & 31) >> 3;
+  unsigned char* pq = base + (c0 >> 5) * chb + q * 128 + (c0 & 7) * 2;
+  *reinterpret_cast<unsigned long long*>(pq + (((2 * g) ^ sw) << 4)) = pl[0];
+  *reinterpret_cast<unsigned long long*>(pq + (((2 * g + 1) ^ sw) << 4)) = pl[1];
 }
 
-// v >= 0 (post-ReLU) scaled by s -> (hi, lo) fp16 planes, round toward zero (split_planes_f16)
-__device__ __forceinline__ void f16_pair(float v, float s, uint16_t& hi, uint16_t& lo) {
-  const float a = v * s;
-  const auto h = __builtin_amdgcn_cvt_pkrtz(a, 0.f);
-  const float r = a - (float)h[0];
-  const auto l = __builtin_amdgcn_cvt_pkrtz(r, 0.f);
-  hi = __builtin_bit_cast(uint16_t, h[0]);
-  lo = __builtin_bit_cast(uint16_t, l[0]);
+// 16 B per lane out through a buffer descriptor (offsets past num_records are dropped)
+__device__ __forceinline__ void bs_f4(__amdgpu_buffer_rsrc_t r, f4 v, unsigned voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, voff, soff, 0);
 }
 
 // B fragments of column block j from a [2 planes][rows][64 B] stage (conv_wave's slot swizzle)
@@ -88,17 +89,18 @@ __device__ __forceinline__ void b_frags(const unsigned char* sb, int rows, int j
   b[1] = *reinterpret_cast<const f16x8*>(bp + rows * 64);
 }
 
-// the three partial products of the split, smallest first (conv_wave.hip's order)
-__device__ __forceinline__ f32x4 mfma3(const f16x8 (&a)[2], const f16x8 (&b)[2], f32x4 c) {
-  c = mfma16(a[1], b[0], c);
-  c = mfma16(a[0], b[1], c);
-  c = mfma16(a[0], b[0], c);
+// the three partial products of the split, smallest first (conv_wave.hip's order), computed
+// transposed: the weight fragment is the MFMA's A operand and the activation fragment its B, so
+// a lane's accumulator holds 4 consecutive CHANNELS of one pixel (16-B epilogue accesses)
+__device__ __forceinline__ f32x4 mfma3t(const f16x8 (&w)[2], const f16x8 (&a)[2], f32x4 c) {
+  c = mfma16(w[0], a[1], c);
+  c = mfma16(w[1], a[0], c);
+  c = mfma16(w[0], a[0], c);
   return c;
 }
 
 __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
-  __shared__ unsigned tmax[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
   int L = xcd_remap(blockIdx.x, p.nwg);
@@ -107,7 +109,6 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   const int th = L % p.tiles_h;
   const int n = L / p.tiles_h;
   const int oh0 = th * TR, ow0 = tw * TC;
-  if (tid < 2) tmax[tid] = 0u;
 
   // ---- descriptors: this frame of x (phase 1 A and the residual), the six weight planes
   const float* xn = p.x + (int64_t)n * p.xsn;
@@ -129,51 +130,52 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
     const unsigned vo = (unsigned)((bnrow * p.kp[l] + bch * 8) * 2);
     bl_lds16(bq ? wr[l][1] : wr[l][0], lds + bdst + stage * STAGE, vo, kt * BK_ * 2);
   };
+  // the W stream: steps u = 0..7 are W1's K-steps, 8..25 W2's; step u goes to stage u % RING
+  constexpr int NK1 = CIO / BK_, NK2 = (MID / 32) * 9, NU = NK1 + NK2;
+  auto issue_wu = [&](int u) {
+    if (u < NK1) issue_w(0, u, u % RING);
+    else if (u < NU) issue_w(1, u - NK1, u % RING);
+  };
 
   // =========================== phase 1: t1 on the haloed tile
   const float am = p.x_amax[n];
   const int ex = f16_scale_exp(am);
   const float sa = ldexpf(1.f, 15 - ex), inv0 = ldexpf(1.f, ex - 15);
-  // row blocks wave and wave + 8 (the latter only for waves 0..3)
+  // row blocks wave and wave + 8 (the latter only for waves 0..3); lane fr's pixel of each
   const bool two = wave + NW < NRB1;                         // wave-uniform
   unsigned av[2];
-  bool pval[2][4];                                           // C-layout rows fg*4 + r: pixel valid
+  bool pv[2];                                                // that pixel is inside the image
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int rb = wave + i * NW;
     const int px = rb * 16 + fr;
     const int hr = px / HW_, hc = px - hr * HW_;
     const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-    const bool ok = px < HP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && rb < NRB1;
-    av[i] = ok ? (unsigned)(((int64_t)ih * p.xsh + (int64_t)iw * p.xsw + fg * 8) * 4) : BL_OOB;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int q = rb * 16 + fg * 4 + r;
-      const int qr = q / HW_, qc = q - qr * HW_;
-      pval[i][r] = q < HP && (unsigned)(oh0 - 1 + qr) < (unsigned)p.H && (unsigned)(ow0 - 1 + qc) < (unsigned)p.W;
-    }
+    pv[i] = px < HP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && rb < NRB1;
+    av[i] = pv[i] ? (unsigned)(((int64_t)ih * p.xsh + (int64_t)iw * p.xsw + fg * 8) * 4) : BL_OOB;
   }
   f32x4 acc1[2][4];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  f4 raw[2][2];
+  // A straight from global into registers, two K-steps ahead (raw[step & 1])
+  f4 raw[2][2][2];
   auto load_a = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (i == 1 && !two) continue;
-      raw[i][0] = bl_f4(xr, av[i], kt * BK_ * 4);
-      raw[i][1] = bl_f4(xr, av[i] + 16, kt * BK_ * 4);
+      raw[kt & 1][i][0] = bl_f4(xr, av[i], kt * BK_ * 4);
+      raw[kt & 1][i][1] = bl_f4(xr, av[i] + 16, kt * BK_ * 4);
     }
   };
   f16x8 af[2][2];
-  auto split = [&]() {
+  auto split = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       unsigned long long p0[2], p1[2];
-      split_planes_f16(raw[i][0], sa, p0);
-      split_planes_f16(raw[i][1], sa, p1);
+      split_planes_f16(raw[kt & 1][i][0], sa, p0);
+      split_planes_f16(raw[kt & 1][i][1], sa, p1);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -181,40 +183,49 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
       }
     }
   };
-  constexpr int NK1 = CIO / BK_;
+  // Per step kt: [wait + barrier] W(kt + RING - 1), A(kt + 2) issued, MFMAs on A(kt), split of
+  // A(kt + 1). The wait leaves in flight exactly the ops issued after this wave's piece of
+  // W(kt) (counted per step below: na = A loads per step), so A stays two steps ahead.
+  static_assert(RING == 4 && NK1 == 8, "phase-1 wait counts");
+#pragma unroll
+  for (int u = 0; u < RING - 1; ++u) issue_wu(u);
   load_a(0);
-  issue_w(0, 0, 0);
-  split();
+  load_a(1);
+  split(0);
+#pragma unroll
   for (int kt = 0; kt < NK1; ++kt) {
-    wait_barrier<0>();
-    if (kt + 1 < NK1) {
-      load_a(kt + 1);
-      issue_w(0, kt + 1, (kt + 1) & 1);
+    // ops issued after W(kt): kt = 0: W1, W2, A0, A1; 1..6: 2 W + 3 A steps (fewer only where the
+    // count is not needed: W(1), W(2) precede A(0)); 7: 2 W + 2 A steps
+    if (two) {
+      if (kt == 0 || kt == NK1 - 1) wait_barrier<2 + 2 * 4>(); else wait_barrier<2 + 3 * 4>();
     } else {
-      issue_w(1, 0, (kt + 1) & 1);                           // W2's first K-step (phase 2)
+      if (kt == 0 || kt == NK1 - 1) wait_barrier<2 + 2 * 2>(); else wait_barrier<2 + 3 * 2>();
     }
-    const unsigned char* sb = lds + RING_OFF + (kt & 1) * STAGE;
+    issue_wu(kt + RING - 1);
+    if (kt + 2 < NK1) load_a(kt + 2);
+    const unsigned char* sb = lds + RING_OFF + (kt % RING) * STAGE;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       f16x8 b[2];
       b_frags(sb, MID, j, fr, fg, b);
-      acc1[0][j] = mfma3(af[0], b, acc1[0][j]);
-      if (two) acc1[1][j] = mfma3(af[1], b, acc1[1][j]);
+      acc1[0][j] = mfma3t(b, af[0], acc1[0][j]);
+      if (two) acc1[1][j] = mfma3t(b, af[1], acc1[1][j]);
     }
-    if (kt + 1 < NK1) split();
+    if (kt + 1 < NK1) split(kt + 1);
   }
-  // epilogue 1: bn1 + ReLU (zero outside the image: conv2's padding), tile max, planes -> TT
+  // epilogue 1: bn1 + ReLU (zero outside the image: conv2's padding), tile max, planes -> TT.
+  // Lane (fr, fg) holds channels j*16 + fg*4 .. +3 of pixel rb*16 + fr.
   float m1 = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = j * 16 + fr;
-    const float s = p.sc[0][c], b = p.bi[0][c];
+    const int c0 = j * 16 + fg * 4;
+    const f4 s = *reinterpret_cast<const f4*>(p.sc[0] + c0), b = *reinterpret_cast<const f4*>(p.bi[0] + c0);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v = fmaf(acc1[i][j][r] * inv0, s, b);
-        v = v > 0.f && pval[i][r] && (i == 0 || two) ? v : 0.f;
+        float v = fmaf(acc1[i][j][r] * inv0, s[r], b[r]);
+        v = v > 0.f && pv[i] && (i == 0 || two) ? v : 0.f;
         acc1[i][j][r] = v;
         m1 = fmaxf(m1, v);
       }
@@ -222,21 +233,25 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m1 = fmaxf(m1, __shfl_xor(m1, o, 64));
   wait_barrier<0>();                                         // every wave's phase-1 reads of the ring done
-  if (lane == 0) atomicMax(&tmax[0], fbits(m1));
+  // tile max through per-wave slots in ring stage 3 (its last content, W1's step 7, is dead
+  // and W(11) is issued only after phase 2's first barrier): no zeroing, no atomics, 80 KB LDS
+  float* const wmax1 = reinterpret_cast<float*>(lds + RING_OFF + 3 * STAGE);
+  if (lane == 0) wmax1[wave] = m1;
   __syncthreads();
-  const int e1 = f16_scale_exp(__builtin_bit_cast(float, tmax[0]));
+  m1 = wmax1[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) m1 = fmaxf(m1, wmax1[w]);
+  const int e1 = f16_scale_exp(m1);
   const float s1 = ldexpf(1.f, 15 - e1), inv1 = ldexpf(1.f, e1 - 15);
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     if (i == 1 && !two) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        uint16_t hi, lo;
-        f16_pair(acc1[i][j][r], s1, hi, lo);
-        put_planes(lds, CHB1, (wave + i * NW) * 16 + fg * 4 + r, j * 16 + fr, hi, lo);
-      }
+    for (int j = 0; j < 4; ++j) {
+      unsigned long long pl[2];
+      split_planes_f16(acc1[i][j], s1, pl);
+      put_planes4(lds, CHB1, (wave + i * NW) * 16 + fr, j * 16 + fg * 4, pl);
+    }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // t1 in LDS before the next barrier
 
@@ -250,39 +265,42 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   f32x4 acc2[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  constexpr int NK2 = (MID / 32) * 9;
-  int kt2 = 0;
+  static_assert(MID / 32 == 2 && RING == 4, "phase-2 wait counts");
+  int u = NK1;
 #pragma unroll 1
   for (int c = 0; c < MID / 32; ++c) {
     const unsigned char* tc = lds + c * CHB1;
 #pragma unroll
-    for (int t = 0; t < 9; ++t, ++kt2) {
-      // K-step k of W2 sits in ring stage k & 1 (its step 0 was issued by phase 1's last step)
-      wait_barrier<0>();
-      if (kt2 + 1 < NK2) issue_w(1, kt2 + 1, (kt2 + 1) & 1);
+    for (int t = 0; t < 9; ++t, ++u) {
+      // W stream step u (its first RING - 1 were issued during phase 1): in flight after this
+      // wave's piece of W(u) are W(u+1), W(u+2) -- fewer in the last two steps
+      if (c == 1 && t >= 7) wait_barrier<0>(); else wait_barrier<RING - 2>();
+      issue_wu(u + RING - 1);
       f16x8 a[2];
       a[0] = *reinterpret_cast<const f16x8*>(tc + aoff[t]);
       a[1] = *reinterpret_cast<const f16x8*>(tc + (aoff[t] ^ 16));
-      const unsigned char* sb = lds + RING_OFF + (kt2 & 1) * STAGE;
+      const unsigned char* sb = lds + RING_OFF + (u % RING) * STAGE;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         f16x8 b[2];
         b_frags(sb, MID, j, fr, fg, b);
-        acc2[j] = mfma3(a, b, acc2[j]);
+        acc2[j] = mfma3t(b, a, acc2[j]);
       }
     }
   }
-  // epilogue 2: bn2 + ReLU, tile max, planes -> TT (t1 is dead once every wave is past here)
-  const int oy = oh0 + wave;
+  // epilogue 2: bn2 + ReLU, tile max, planes -> TT (t1 is dead once every wave is past here).
+  // Lane (fr, fg): output pixel (oh0 + wave, ow0 + fr), channels j*16 + fg*4 .. +3.
+  const int oy = oh0 + wave, ox = ow0 + fr;
+  const bool ov = oy < p.H && ox < p.W;
   float m2 = 0.f;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int c = j * 16 + fr;
-    const float s = p.sc[1][c], b = p.bi[1][c];
+    const int c0 = j * 16 + fg * 4;
+    const f4 s = *reinterpret_cast<const f4*>(p.sc[1] + c0), b = *reinterpret_cast<const f4*>(p.bi[1] + c0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float v = fmaf(acc2[j][r] * inv1, s, b);
-      v = v > 0.f && oy < p.H && ow0 + fg * 4 + r < p.W ? v : 0.f;
+      float v = fmaf(acc2[j][r] * inv1, s[r], b[r]);
+      v = v > 0.f && ov ? v : 0.f;
       acc2[j][r] = v;
       m2 = fmaxf(m2, v);
     }
@@ -290,7 +308,8 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m2 = fmaxf(m2, __shfl_xor(m2, o, 64));
   wait_barrier<0>();                                         // all t1 / W2 reads done, TT and ring free
-  if (lane == 0) atomicMax(&tmax[1], fbits(m2));
+  float* const wmax2 = reinterpret_cast<float*>(lds + RING_OFF + 2 * STAGE);   // past the W3 overlay
+  if (lane == 0) wmax2[wave] = m2;
   // W3 half 0 into the overlay (TT's last 16 KB + the ring): 32 pieces, 4 per wave
   auto issue_w3 = [&](int h) {
 #pragma unroll
@@ -305,32 +324,39 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   };
   issue_w3(0);
   __syncthreads();
-  const int e2 = f16_scale_exp(__builtin_bit_cast(float, tmax[1]));
+  m2 = wmax2[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) m2 = fmaxf(m2, wmax2[w]);
+  const int e2 = f16_scale_exp(m2);
   const float s2 = ldexpf(1.f, 15 - e2), inv2 = ldexpf(1.f, e2 - 15);
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      uint16_t hi, lo;
-      f16_pair(acc2[j][r], s2, hi, lo);
-      put_planes(lds, CHB2, wave * 16 + fg * 4 + r, j * 16 + fr, hi, lo);
-    }
+  for (int j = 0; j < 4; ++j) {
+    unsigned long long pl[2];
+    split_planes_f16(acc2[j], s2, pl);
+    put_planes4(lds, CHB2, wave * 16 + fr, j * 16 + fg * 4, pl);
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // t2 in LDS before the next barrier
 
-  // =========================== phase 3: y = relu(bn3(W3 t2) + x), two halves of 128 columns
+  // =========================== phase 3: y = relu(bn3(W3 t2) + x), two halves of 128 columns.
+  // Residual loads and y stores are 16-B buffer accesses (an invalid pixel's offset is past the
+  // descriptor: zeros / dropped), issued unconditionally so every wave counts the same vmcnt.
+  const int yframe_bytes = (int)(((int64_t)(p.H - 1) * p.ysh + (int64_t)(p.W - 1) * p.ysw + CIO) * 4);
+  const __amdgpu_buffer_rsrc_t yr = buf_rsrc(p.y + (int64_t)n * p.ysn, yframe_bytes);
+  const unsigned rvo = ov ? (unsigned)(((int64_t)oy * p.xsh + (int64_t)ox * p.xsw + fg * 4) * 4) : BL_OOB;
+  const unsigned yvo = ov ? (unsigned)(((int64_t)oy * p.ysh + (int64_t)ox * p.ysw + fg * 4) * 4) : BL_OOB;
   const int q3 = wave * 16 + fr;
   const int a3 = q3 * 128 + (((2 * fg) ^ ((q3 >> 1) & 7)) << 4);
   float ymax = 0.f;
+  f4 res[8];
 #pragma unroll 1
   for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) res[j] = bl_f4(xr, rvo, (h * 128 + j * 16) * 4);
     if (h == 0) {
-      wait_barrier<0>();                                     // W3 half 0 landed, t2 written
-    } else if (oy < p.H) {
-      // W3 half 1 was issued before half 0's residual loads and stores (<= 64 younger ops):
-      // leaving the 32 youngest in flight still covers it; then publish every wave's pieces
-      asm volatile("s_waitcnt vmcnt(32)\n\ts_barrier" ::: "memory");
+      wait_barrier<8>();                                     // t2 written (W3 half 0 landed at the __syncthreads)
     } else {
-      wait_barrier<0>();                                     // a wave with no valid row issued nothing after it
+      // W3 half 1 was issued before half 0's 8 stores and this half's 8 residual loads
+      wait_barrier<16>();
     }
     f32x4 acc3[8];
 #pragma unroll
@@ -345,33 +371,33 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
       for (int j = 0; j < 8; ++j) {
         f16x8 b[2];
         b_frags(sb, 128, j, fr, fg, b);
-        acc3[j] = mfma3(a, b, acc3[j]);
+        acc3[j] = mfma3t(b, a, acc3[j]);
       }
     }
     if (h == 0) {
       // every wave is done reading W3 half 0 (its ds_reads fed the MFMAs above): overwrite it
-      // with half 1 now, BEFORE this half's residual loads and stores
-      asm volatile("s_barrier" ::: "memory");
+      // with half 1 now, BEFORE this half's stores
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       issue_w3(1);
       asm volatile("" ::: "memory");
     }
-    // residual + bn3 + ReLU, stored from the accumulator layout (16 channels = 64 B per row)
+    // residual + bn3 + ReLU: lane (fr, fg) = pixel (oy, ox), channels h*128 + j*16 + fg*4 .. +3
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int c = h * 128 + j * 16 + fr;
-      const float s = p.sc[2][c], b = p.bi[2][c];
+      const int c0 = h * 128 + j * 16 + fg * 4;
+      const f4 s = *reinterpret_cast<const f4*>(p.sc[2] + c0), b = *reinterpret_cast<const f4*>(p.bi[2] + c0);
+      f4 v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int ox = ow0 + fg * 4 + r;
-        if (oy >= p.H || ox >= p.W) continue;
-        const float res = xn[(int64_t)oy * p.xsh + (int64_t)ox * p.xsw + c];
-        float v = fmaf(acc3[j][r] * inv2, s, b) + res;
-        v = v > 0.f ? v : 0.f;
-        p.y[(int64_t)n * p.ysn + (int64_t)oy * p.ysh + (int64_t)ox * p.ysw + c] = v;
-        ymax = fmaxf(ymax, v);
+        const float t = fmaf(acc3[j][r] * inv2, s[r], b[r]) + res[j][r];
+        v[r] = t > 0.f ? t : 0.f;
+        ymax = fmaxf(ymax, v[r]);
       }
+      bs_f4(yr, v, yvo, (h * 128 + j * 16) * 4);
     }
+    asm volatile("" ::: "memory");
   }
+  if (!ov) ymax = 0.f;                                       // (an invalid pixel's y is relu(bias))
   if (p.y_amax) amax_commit(p.y_amax + n, ymax);
 }
 
@@ -396,14 +422,18 @@ extern "C" int prpe_bottleneck(const prpe_bneck_desc* d, void* stream) {
   const prpe_view& x = d->x; const prpe_view& y = d->y;
   if (d->mid != MID || x.c != CIO || y.c != CIO || x.n != y.n || x.h != y.h || x.w != y.w) return PRPE_EINVAL;
   if (x.sc != 1 || y.sc != 1 || x.sw % 4 || x.sh % 4 || x.sn % 4 || (uintptr_t)x.ptr % 16 || x.sw < 0 || x.sh < 0 ||
-      y.sw < 0 || y.sh < 0)
+      y.sw % 4 || y.sh % 4 || y.sn % 4 || (uintptr_t)y.ptr % 16 || y.sw < 0 || y.sh < 0)
     return PRPE_EINVAL;
   const int kneed[3] = {CIO, 9 * MID, MID};
   for (int l = 0; l < 3; ++l) {
     if (!d->w_h16[l] || !d->w_l16[l] || !d->scale16[l] || !d->bias[l] || d->k_pad[l] != kneed[l]) return PRPE_EINVAL;
-    if ((uintptr_t)d->w_h16[l] % 16 || (uintptr_t)d->w_l16[l] % 16) return PRPE_EINVAL;
+    if ((uintptr_t)d->w_h16[l] % 16 || (uintptr_t)d->w_l16[l] % 16 || (uintptr_t)d->scale16[l] % 16 ||
+        (uintptr_t)d->bias[l] % 16)
+      return PRPE_EINVAL;
   }
-  if (((int64_t)(x.h - 1) * x.sh + (int64_t)(x.w - 1) * x.sw + CIO) * 4 >= (1LL << 31)) return PRPE_EINVAL;
+  if (((int64_t)(x.h - 1) * x.sh + (int64_t)(x.w - 1) * x.sw + CIO) * 4 >= (1LL << 31) ||
+      ((int64_t)(y.h - 1) * y.sh + (int64_t)(y.w - 1) * y.sw + CIO) * 4 >= (1LL << 31))
+    return PRPE_EINVAL;
   BneckK kp{};
   kp.x = x.ptr; kp.xsn = x.sn; kp.xsh = x.sh; kp.xsw = x.sw; kp.x_amax = d->x_amax;
   kp.y = y.ptr; kp.ysn = y.sn; kp.ysh = y.sh; kp.ysw = y.sw; kp.y_amax = d->y_amax;

@@ -446,12 +446,13 @@ int launch_halo_kind(const ConvK& kp, int prec, hipStream_t st) {
                      : launch_halo<NW, TR, TC, TN, false, false, 0, WN>(kp, st);
 }
 
-// epilogue tap GEMM: the 8 x 16-pixel, 128-column tile
-template <int TAPS, int WN>
+// epilogue tap GEMM: the 8 x 16-pixel, 128-column tile (NW = 4) or the 16 x 16 one (NW = 8)
+template <int TAPS, int WN, int NW = 4>
 int launch_halo_taps_t(const ConvK& kp, int prec, hipStream_t st) {
-  if (prec == 3) return launch_halo<4, 8, 16, 8, true, false, TAPS, WN>(kp, st);
-  return kp.x_planes ? launch_halo<4, 8, 16, 8, false, true, TAPS, WN>(kp, st)
-                     : launch_halo<4, 8, 16, 8, false, false, TAPS, WN>(kp, st);
+  constexpr int TR = NW == 4 ? 8 : 16;
+  if (prec == 3) return launch_halo<NW, TR, 16, 8, true, false, TAPS, WN>(kp, st);
+  return kp.x_planes ? launch_halo<NW, TR, 16, 8, false, true, TAPS, WN>(kp, st)
+                     : launch_halo<NW, TR, 16, 8, false, false, TAPS, WN>(kp, st);
 }
 // PRPE_HALO_WN=2: the 2 x 2 wave grid (WN = 2) for the automatic and epilogue-GEMM tiles.
 // Off by default: in the model at bs = 256 it measured ViT adapter.7 +0.6 %, face-YOLO .10
@@ -501,7 +502,10 @@ bool conv_halo_auto(const ConvK& kp, int prec) {
 // per workgroup, or 64 when Co <= 64 (tools/conv_bench.py, profiles/r02_conv_bench_halo.txt);
 // 31..35 force a configuration
 int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
-  if (kp.w2) return tile == 30 || tile == 31 ? launch_halo_taps(kp, prec, st) : PRPE_EINVAL;
+  if (kp.w2) {
+    if (tile == 32) return kp.w3 ? launch_halo_taps_t<2, 1, 8>(kp, prec, st) : launch_halo_taps_t<1, 1, 8>(kp, prec, st);
+    return tile == 30 || tile == 31 ? launch_halo_taps(kp, prec, st) : PRPE_EINVAL;
+  }
   if (tile == 30) tile = kp.Co <= 64 ? 34 : (halo_wn() == 2 ? 36 : 31);
   switch (tile) {
     case 31: return launch_halo_kind<4, 8, 16, 8>(kp, prec, st);     // 8 x 16 px, 4 waves, 128 ch
