@@ -227,7 +227,9 @@ __global__ __launch_bounds__(AL / 16 / QT * 64) __attribute__((amdgpu_waves_per_
   }
 
   for (int c0 = 0; c0 < AL; c0 += KC) {
+    __builtin_amdgcn_sched_barrier(0);     // the previous chunk's reads stay above the barrier,
     if (c0) __syncthreads();               // every wave done with the previous chunk
+    __builtin_amdgcn_sched_barrier(0);     // this chunk's below it
     // K rows [key][d] as hi/lo: one float4 per item, 8-B LDS writes
     for (int i = tid; i < KC * (AD / 4); i += NT) {
       const int key = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
@@ -266,7 +268,9 @@ __global__ __launch_bounds__(AL / 16 / QT * 64) __attribute__((amdgpu_waves_per_
         *reinterpret_cast<bf16x4*>(Vl + (d4 + dd) * VR + k4 * 4) = vlo;
       }
     }
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
 
     // S^T tiles: rows = keys c0 + 16 t + 4 fg + r, column = query q0 + 16 u + fr
     f32x4 s[QT][KT];

@@ -108,12 +108,17 @@ __device__ __forceinline__ f4 bl_f4(__amdgpu_buffer_rsrc_t r, unsigned voff, int
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, soff, 0));
 }
 
-// s_waitcnt vmcnt(N) + s_barrier in one asm statement with a memory clobber: no LDS access
-// may be moved across it, and it does not drain the LDS-DMA copies still in flight (a
-// __syncthreads() would emit vmcnt(0) here)
+// s_waitcnt vmcnt(N) + s_barrier in one asm statement with a memory clobber, fenced by
+// sched_barrier(0) on both sides. It does not drain the LDS-DMA copies still in flight (a
+// __syncthreads() would emit vmcnt(0) here). The memory clobber alone does not stop the machine
+// scheduler: it hoisted the next K-step's ds_reads above the s_barrier in conv_bneck.hip, i.e.
+// a wave read a ring stage before the other waves' DMA pieces of it were known to have landed
+// (a race: run-to-run differences at bs = 256; tools/barrier_hoist_check.py finds such reads).
 template <int N>
 __device__ __forceinline__ void wait_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+  __builtin_amdgcn_sched_barrier(0);
 }
 
 // direct global->LDS kernel (conv_glds.hip): Ci % 32 == 0 channel-contiguous input, chunk-major

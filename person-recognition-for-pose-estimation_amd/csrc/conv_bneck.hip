@@ -377,7 +377,9 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
     if (h == 0) {
       // every wave is done reading W3 half 0 (its ds_reads fed the MFMAs above): overwrite it
       // with half 1 now, BEFORE this half's stores
+      __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
       issue_w3(1);
       asm volatile("" ::: "memory");
     }

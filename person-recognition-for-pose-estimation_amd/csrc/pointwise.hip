@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
   int issued = __builtin_amdgcn_readfirstlane(hi_at(oy0));
   for (int r = __builtin_amdgcn_readfirstlane(lo_row); r <= issued; ++r) issue_row(r);
   if (issued + 1 < Hi) issue_row(++issued);           // one row ahead
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+  { __builtin_amdgcn_sched_barrier(0); asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); __builtin_amdgcn_sched_barrier(0); }
   int in_use = hi_at(oy0);
 
   const int yo = ox * (int)p.y.sw + (c0 + cg * 4) * (int)p.y.sc;
@@ -387,9 +387,9 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
       // the row(s) coming into use were DMA'd at the previous such event, >= UPD_MIN output rows
       // (stores) ago: wait for everything older than those stores, then publish every wave's
       // pieces. A wave with no live column issues no stores: it waits for all of its DMA.
-      if (!wlive) asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      else if constexpr (PL) asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory");
+      if (!wlive) { __builtin_amdgcn_sched_barrier(0); asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory"); __builtin_amdgcn_sched_barrier(0); }
+      else if constexpr (PL) { __builtin_amdgcn_sched_barrier(0); asm volatile("s_waitcnt vmcnt(8)\n\ts_barrier" ::: "memory"); __builtin_amdgcn_sched_barrier(0); }
+      else { __builtin_amdgcn_sched_barrier(0); asm volatile("s_waitcnt vmcnt(4)\n\ts_barrier" ::: "memory"); __builtin_amdgcn_sched_barrier(0); }
       in_use = need;
       while (issued < need + 1 && issued + 1 < Hi) issue_row(++issued);   // one row ahead again
     }

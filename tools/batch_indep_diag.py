@@ -1,0 +1,85 @@
+"""Diagnostic (GPU box): where does frame f of a bs=B forward stop being bit-identical to the
+same frame run at bs=2? Records every conv / fused-bottleneck output of the selected frame in
+call order for both runs and prints the first mismatching layer (tests/test_gpu_batch.py
+test_frames_independent_of_batch_bit_identical)."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "person-recognition-for-pose-estimation_amd")]
+
+import torch  # noqa: E402
+
+from prpe import arch, synth  # noqa: E402
+from prpe import engine as E  # noqa: E402
+
+STRIDE = [8.0, 16.0, 32.0]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--frame", type=int, default=127)
+    ap.add_argument("--concurrent", type=int, default=0)
+    a = ap.parse_args()
+    sd = synth.make_state_dict(arch.state_dict_spec())
+    from prpe import CombinedModel
+    model = CombinedModel(sd, device="cuda")
+    rec = []
+    sel = [0]
+    conv0, bn0, up0 = E.Engine.conv, E.Engine.bottleneck, E.Engine.upconv
+
+    def conv(self, x, p, *args, **kw):
+        y = conv0(self, x, p, *args, **kw)
+        rec.append((p.name, y[sel[0]].detach().float().cpu().clone()))
+        return y
+
+    def bneck(self, q, x):
+        y = bn0(self, q, x)
+        rec.append((q + ":x_amax", x._prpe_amax[sel[0]:sel[0] + 1].detach().cpu().clone()))
+        rec.append((q, y[sel[0]].detach().cpu().clone()))
+        rec.append((q + ":y_amax", y._prpe_amax[sel[0]:sel[0] + 1].detach().cpu().clone()))
+        return y
+
+    def upconv(self, name, *args, **kw):
+        y = up0(self, name, *args, **kw)
+        rec.append((name + ":up", y[sel[0]].detach().float().cpu().clone()))
+        return y
+
+    E.Engine.conv, E.Engine.bottleneck, E.Engine.upconv = conv, bneck, upconv
+    x = synth.frames(a.batch)
+    runs = []
+    for xb, fi in ((x, a.frame), (x, a.frame), (x[[0, a.frame]], 1)):
+        rec.clear()
+        sel[0] = fi
+        with torch.no_grad():
+            model.forward_all(xb.cuda(), face_stride=STRIDE, concurrent=bool(a.concurrent))
+        torch.cuda.synchronize()
+        runs.append(list(rec))
+    for title, A, B in (("bs=B run twice (determinism)", runs[0], runs[1]), ("bs=B vs bs=2", runs[0], runs[2])):
+        print(f"== {title}: concurrent={a.concurrent} bs={a.batch} frame {a.frame}: {len(A)} / {len(B)} outputs",
+              flush=True)
+        compare(A, B)
+
+
+def compare(A, B):
+    nbad = 0
+    for (na, ta), (nb, tb) in zip(A, B):
+        if na != nb or ta.shape != tb.shape:
+            print("call order differs:", na, nb, ta.shape, tb.shape)
+            break
+        if na.startswith("vit_pose.vit_pose"):
+            continue                      # [B*L, 1, 1, D] linears: row sel is a token, not a frame
+        if not torch.equal(ta, tb):
+            d = (ta - tb).abs()
+            print(f"MISMATCH {na:50s} max|d|={d.max():.3e} n={int((d > 0).sum())}/{d.numel()} "
+                  f"max|y|={tb.abs().max():.3e}", flush=True)
+            nbad += 1
+            if nbad >= 12:
+                break
+    print("first mismatches listed:", nbad, flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 3 (session 2): full GPU suite + smoke + per-layer profile + bench on the current tree
+set -o pipefail
+O=gpurun_out
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/r03h_gpu_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/r03h_smoke.log 2>&1 || exit 2
+timeout -k 10 300 python tools/layer_profile.py --batch 256 --top 300 > $O/r03h_layer_profile.txt 2>&1 || exit 3
+timeout -k 10 400 python bench.py --steps 20 --warmup 3 > $O/r03h_bench.json 2> $O/r03h_bench.err || exit 4
