@@ -46,12 +46,14 @@ struct BneckK {
   int kp[3];
   const float* sc[3]; const float* bi[3];
   int tiles_w, tiles_h, nwg;
+  int proj;                                              // x has MID channels (layer1.0, see BShape)
 };
 
 namespace {
 
 constexpr int BK_ = 32;
-constexpr int MID = 64, CIO = 256, TR = 8, TC = 16, NW = 8;
+constexpr int MID = 64, CIO = 256, TR = 8, TC = 16, NW = 8;     // CIO: output channels (and the
+                                                                 // identity block's input)
 constexpr int HW_ = TC + 2, HP = (TR + 2) * HW_;        // 18, 180 haloed pixels
 constexpr int NRB1 = (HP + 15) / 16;                     // 12 row blocks of haloed pixels
 constexpr int CHB1 = NRB1 * 16 * 128;                    // bytes of one 32-channel chunk of t1
@@ -60,10 +62,25 @@ constexpr int TT_BYTES = (MID / 32) * CHB1;              // 48 KB
 constexpr int STAGE = 2 * MID * 64;                      // one K-step of W1 / W2 (both planes)
 constexpr int RING_OFF = TT_BYTES;
 constexpr int W3_OFF = (MID / 32) * CHB2;                // 32 KB: after t2
-constexpr int W3_STEP = 2 * 128 * 64;                    // one K-step of a W3 half (both planes)
+constexpr int W3_PART = 32 * 1024;                       // one W3 part (below) in the overlay
 constexpr int RING = 4;                                  // W1 / W2 ring stages (3 K-steps of lookahead)
 constexpr int LDS_BYTES = TT_BYTES + RING * STAGE;       // 80 KB: two workgroups per CU
-static_assert(W3_OFF + (MID / 32) * W3_STEP <= RING_OFF + 2 * STAGE, "W3 half overlay below ring stage 2");
+static_assert(W3_OFF + W3_PART <= RING_OFF + 2 * STAGE, "W3 part overlay below ring stage 2");
+
+// Block shape. Identity (layer1.1 / 1.2): x has CIO channels and is the residual; conv3 (K =
+// MID) runs in two parts of 128 output columns. Projection (PROJ, layer1.0): x has MID channels,
+// conv3 and the downsample projection are one dual GEMM over [t2 | x] (the engine's pk_dual pack,
+// K = 2 MID, W' = [s3 W3 | sd Wd]), run in four parts of 64 columns; no residual read.
+template <bool PROJ> struct BShape {
+  static constexpr int CIN = PROJ ? MID : CIO;           // x channels
+  static constexpr int NK1 = CIN / BK_;                  // phase-1 K-steps
+  static constexpr int NKS3 = PROJ ? 2 * MID / BK_ : MID / BK_;   // phase-3 K-steps
+  static constexpr int R3 = PROJ ? 64 : 128;             // output columns per phase-3 part
+  static constexpr int NPART = CIO / R3;
+  static constexpr int W3_STEP = 2 * R3 * 64;            // one K-step of a part (both planes)
+  static_assert(NKS3 * W3_STEP == W3_PART, "W3 part size");
+  static_assert(NKS3 * 2 * (R3 / 16) == 4 * NW, "4 W3 pieces per wave and part");
+};
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
@@ -99,7 +116,10 @@ __device__ __forceinline__ f32x4 mfma3t(const f16x8 (&w)[2], const f16x8 (&a)[2]
   return c;
 }
 
+template <bool PROJ>
 __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
+  using S = BShape<PROJ>;
+  constexpr int CIN = S::CIN, NK1 = S::NK1, R3 = S::R3, W3_STEP = S::W3_STEP;
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
@@ -112,7 +132,7 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
 
   // ---- descriptors: this frame of x (phase 1 A and the residual), the six weight planes
   const float* xn = p.x + (int64_t)n * p.xsn;
-  const int frame_bytes = (int)(((int64_t)(p.H - 1) * p.xsh + (int64_t)(p.W - 1) * p.xsw + CIO) * 4);
+  const int frame_bytes = (int)(((int64_t)(p.H - 1) * p.xsh + (int64_t)(p.W - 1) * p.xsw + CIN) * 4);
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc(xn, frame_bytes);
   __amdgpu_buffer_rsrc_t wr[3][2];
 #pragma unroll
@@ -130,8 +150,8 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
     const unsigned vo = (unsigned)((bnrow * p.kp[l] + bch * 8) * 2);
     bl_lds16(bq ? wr[l][1] : wr[l][0], lds + bdst + stage * STAGE, vo, kt * BK_ * 2);
   };
-  // the W stream: steps u = 0..7 are W1's K-steps, 8..25 W2's; step u goes to stage u % RING
-  constexpr int NK1 = CIO / BK_, NK2 = (MID / 32) * 9, NU = NK1 + NK2;
+  // the W stream: steps u < NK1 are W1's K-steps, the next 18 W2's; step u goes to stage u % RING
+  constexpr int NK2 = (MID / 32) * 9, NU = NK1 + NK2;
   auto issue_wu = [&](int u) {
     if (u < NK1) issue_w(0, u, u % RING);
     else if (u < NU) issue_w(1, u - NK1, u % RING);
@@ -186,7 +206,7 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   // Per step kt: [wait + barrier] W(kt + RING - 1), A(kt + 2) issued, MFMAs on A(kt), split of
   // A(kt + 1). The wait leaves in flight exactly the ops issued after this wave's piece of
   // W(kt) (counted per step below: na = A loads per step), so A stays two steps ahead.
-  static_assert(RING == 4 && NK1 == 8, "phase-1 wait counts");
+  static_assert(RING == 4 && NK1 >= 2, "phase-1 wait counts");
 #pragma unroll
   for (int u = 0; u < RING - 1; ++u) issue_wu(u);
   load_a(0);
@@ -194,8 +214,8 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   split(0);
 #pragma unroll
   for (int kt = 0; kt < NK1; ++kt) {
-    // ops issued after W(kt): kt = 0: W1, W2, A0, A1; 1..6: 2 W + 3 A steps (fewer only where the
-    // count is not needed: W(1), W(2) precede A(0)); 7: 2 W + 2 A steps
+    // ops issued after W(kt): kt = 0: W1, W2, A0, A1; middle steps: 2 W + 3 A steps (fewer only
+    // where the count is not needed: W(1), W(2) precede A(0)); last: 2 W + 2 A steps
     if (two) {
       if (kt == 0 || kt == NK1 - 1) wait_barrier<2 + 2 * 4>(); else wait_barrier<2 + 3 * 4>();
     } else {
@@ -233,9 +253,9 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m1 = fmaxf(m1, __shfl_xor(m1, o, 64));
   wait_barrier<0>();                                         // every wave's phase-1 reads of the ring done
-  // tile max through per-wave slots in ring stage 3 (its last content, W1's step 7, is dead
-  // and W(11) is issued only after phase 2's first barrier): no zeroing, no atomics, 80 KB LDS
-  float* const wmax1 = reinterpret_cast<float*>(lds + RING_OFF + 3 * STAGE);
+  // tile max through per-wave slots in the ring stage of W1's last step (dead now; the next DMA
+  // into it, W(NK1 + 3), is issued only after phase 2's first barrier): no zeroing, no atomics
+  float* const wmax1 = reinterpret_cast<float*>(lds + RING_OFF + ((NK1 - 1) % RING) * STAGE);
   if (lane == 0) wmax1[wave] = m1;
   __syncthreads();
   m1 = wmax1[0];
@@ -310,16 +330,30 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   wait_barrier<0>();                                         // all t1 / W2 reads done, TT and ring free
   float* const wmax2 = reinterpret_cast<float*>(lds + RING_OFF + 2 * STAGE);   // past the W3 overlay
   if (lane == 0) wmax2[wave] = m2;
-  // W3 half 0 into the overlay (TT's last 16 KB + the ring): 32 pieces, 4 per wave
+  // PROJ: the downsample operand, x at this lane's output pixel (channels ks*32 + fg*8 .. +7),
+  // loaded now (older than every W3 piece, so the counted waits below stay exact)
+  constexpr int NXK = PROJ ? MID / BK_ : 1;
+  f4 xc[NXK][2];
+  if constexpr (PROJ) {
+    const unsigned cvo = ov ? (unsigned)(((int64_t)oy * p.xsh + (int64_t)ox * p.xsw + fg * 8) * 4) : BL_OOB;
+#pragma unroll
+    for (int ks = 0; ks < NXK; ++ks) {
+      xc[ks][0] = bl_f4(xr, cvo, ks * BK_ * 4);
+      xc[ks][1] = bl_f4(xr, cvo + 16, ks * BK_ * 4);
+    }
+  }
+  // W3 part h (R3 output columns, all NKS3 K-steps, both planes) into the overlay (TT's last
+  // 16 KB + ring stages 0-1): 32 pieces, 4 per wave
   auto issue_w3 = [&](int h) {
+    constexpr int RB3 = R3 / 16;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = wave * 4 + i;
-      const int ks = idx >> 4, q = (idx >> 3) & 1, rb = idx & 7;
+      const int rb = idx % RB3, q = (idx / RB3) & 1, ks = idx / (2 * RB3);
       const int nrow = rb * 16 + (lane >> 2);
       const int ch = (lane & 3) ^ swzF(nrow);
-      const unsigned vo = (unsigned)(((h * 128 + nrow) * p.kp[2] + ch * 8) * 2);
-      bl_lds16(q ? wr[2][1] : wr[2][0], lds + W3_OFF + ks * W3_STEP + (q * 128 + rb * 16) * 64, vo, ks * BK_ * 2);
+      const unsigned vo = (unsigned)(((h * R3 + nrow) * p.kp[2] + ch * 8) * 2);
+      bl_lds16(q ? wr[2][1] : wr[2][0], lds + W3_OFF + ks * W3_STEP + (q * R3 + rb * 16) * 64, vo, ks * BK_ * 2);
     }
   };
   issue_w3(0);
@@ -327,7 +361,9 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   m2 = wmax2[0];
 #pragma unroll
   for (int w = 1; w < NW; ++w) m2 = fmaxf(m2, wmax2[w]);
-  const int e2 = f16_scale_exp(m2);
+  // PROJ: t2 and x feed one accumulator, so they share one scale (their maxima combined, as
+  // prpe_conv2d's dual-input GEMM); the x bound is per frame, t2's per tile
+  const int e2 = f16_scale_exp(PROJ ? fmaxf(m2, am) : m2);
   const float s2 = ldexpf(1.f, 15 - e2), inv2 = ldexpf(1.f, e2 - 15);
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -336,10 +372,27 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
     put_planes4(lds, CHB2, wave * 16 + fr, j * 16 + fg * 4, pl);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // t2 in LDS before the next barrier
+  f16x8 xb[NXK][2];
+  if constexpr (PROJ) {
+#pragma unroll
+    for (int ks = 0; ks < NXK; ++ks) {
+      unsigned long long p0[2], p1[2];
+      split_planes_f16(xc[ks][0], s2, p0);
+      split_planes_f16(xc[ks][1], s2, p1);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        xb[ks][q] = __builtin_bit_cast(f16x8, u64x2{p0[q], p1[q]});
+      }
+    }
+  }
 
-  // =========================== phase 3: y = relu(bn3(W3 t2) + x), two halves of 128 columns.
-  // Residual loads and y stores are 16-B buffer accesses (an invalid pixel's offset is past the
-  // descriptor: zeros / dropped), issued unconditionally so every wave counts the same vmcnt.
+  // =========================== phase 3: y = relu(bn3(W3 t2) + x) in NPART parts of R3 columns
+  // (PROJ: y = relu(W' [t2 | x] + b3 + bd)). Residual loads and y stores are 16-B buffer
+  // accesses (an invalid pixel's offset is past the descriptor: zeros / dropped), issued
+  // unconditionally so every wave counts the same vmcnt.
+  constexpr int NPART = S::NPART, NKS3 = S::NKS3, NJ = R3 / 16;
+  constexpr int NRES = PROJ ? 0 : NJ;                        // residual loads per part
   const int yframe_bytes = (int)(((int64_t)(p.H - 1) * p.ysh + (int64_t)(p.W - 1) * p.ysw + CIO) * 4);
   const __amdgpu_buffer_rsrc_t yr = buf_rsrc(p.y + (int64_t)n * p.ysn, yframe_bytes);
   const unsigned rvo = ov ? (unsigned)(((int64_t)oy * p.xsh + (int64_t)ox * p.xsw + fg * 4) * 4) : BL_OOB;
@@ -347,55 +400,63 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   const int q3 = wave * 16 + fr;
   const int a3 = q3 * 128 + (((2 * fg) ^ ((q3 >> 1) & 7)) << 4);
   float ymax = 0.f;
-  f4 res[8];
+  f4 res[PROJ ? 1 : NJ];
 #pragma unroll 1
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < NPART; ++h) {
+    if constexpr (!PROJ) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) res[j] = bl_f4(xr, rvo, (h * 128 + j * 16) * 4);
-    if (h == 0) {
-      wait_barrier<8>();                                     // t2 written (W3 half 0 landed at the __syncthreads)
-    } else {
-      // W3 half 1 was issued before half 0's 8 stores and this half's 8 residual loads
-      wait_barrier<16>();
+      for (int j = 0; j < NJ; ++j) res[j] = bl_f4(xr, rvo, (h * R3 + j * 16) * 4);
     }
-    f32x4 acc3[8];
+    if (h == 0) {
+      wait_barrier<NRES>();                                  // t2 written (W3 part 0 landed at the __syncthreads)
+    } else {
+      // W3 part h was issued before part h-1's NJ stores and this part's residual loads
+      wait_barrier<NJ + NRES>();
+    }
+    f32x4 acc3[NJ];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc3[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc3[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < MID / 32; ++ks) {
+    for (int ks = 0; ks < NKS3; ++ks) {
       f16x8 a[2];
-      a[0] = *reinterpret_cast<const f16x8*>(lds + ks * CHB2 + a3);
-      a[1] = *reinterpret_cast<const f16x8*>(lds + ks * CHB2 + (a3 ^ 16));
+      if (ks < MID / BK_) {
+        a[0] = *reinterpret_cast<const f16x8*>(lds + ks * CHB2 + a3);
+        a[1] = *reinterpret_cast<const f16x8*>(lds + ks * CHB2 + (a3 ^ 16));
+      } else {
+        a[0] = xb[ks - MID / BK_ < NXK ? ks - MID / BK_ : 0][0];
+        a[1] = xb[ks - MID / BK_ < NXK ? ks - MID / BK_ : 0][1];
+      }
       const unsigned char* sb = lds + W3_OFF + ks * W3_STEP;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         f16x8 b[2];
-        b_frags(sb, 128, j, fr, fg, b);
+        b_frags(sb, R3, j, fr, fg, b);
         acc3[j] = mfma3t(b, a, acc3[j]);
       }
     }
-    if (h == 0) {
-      // every wave is done reading W3 half 0 (its ds_reads fed the MFMAs above): overwrite it
-      // with half 1 now, BEFORE this half's stores
+    if (h + 1 < NPART) {
+      // every wave is done reading W3 part h (its ds_reads fed the MFMAs above): overwrite it
+      // with part h + 1 now, BEFORE this part's stores
       __builtin_amdgcn_sched_barrier(0);
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
-      issue_w3(1);
+      issue_w3(h + 1);
       asm volatile("" ::: "memory");
     }
-    // residual + bn3 + ReLU: lane (fr, fg) = pixel (oy, ox), channels h*128 + j*16 + fg*4 .. +3
+    // (residual +) bn3 + ReLU: lane (fr, fg) = pixel (oy, ox), channels h*R3 + j*16 + fg*4 .. +3
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int c0 = h * 128 + j * 16 + fg * 4;
+    for (int j = 0; j < NJ; ++j) {
+      const int c0 = h * R3 + j * 16 + fg * 4;
       const f4 s = *reinterpret_cast<const f4*>(p.sc[2] + c0), b = *reinterpret_cast<const f4*>(p.bi[2] + c0);
       f4 v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float t = fmaf(acc3[j][r] * inv2, s[r], b[r]) + res[j][r];
+        float t = fmaf(acc3[j][r] * inv2, s[r], b[r]);
+        if constexpr (!PROJ) t += res[j][r];
         v[r] = t > 0.f ? t : 0.f;
         ymax = fmaxf(ymax, v[r]);
       }
-      bs_f4(yr, v, yvo, (h * 128 + j * 16) * 4);
+      bs_f4(yr, v, yvo, (h * R3 + j * 16) * 4);
     }
     asm volatile("" ::: "memory");
   }
@@ -412,7 +473,8 @@ int bneck_launch(const BneckK& kp0, hipStream_t st) {
   const int64_t nwg = (int64_t)kp.N * kp.tiles_w * kp.tiles_h;
   if (nwg <= 0 || nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
-  hipLaunchKernelGGL(bneck_kernel, dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  if (kp.proj) hipLaunchKernelGGL(bneck_kernel<true>, dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  else hipLaunchKernelGGL(bneck_kernel<false>, dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
   return launch_status();
 }
 
@@ -422,24 +484,27 @@ extern "C" int prpe_bottleneck(const prpe_bneck_desc* d, void* stream) {
   using namespace prpe_k;
   if (!d || !view_ok(&d->x) || !view_ok(&d->y) || !d->x_amax) return PRPE_EINVAL;
   const prpe_view& x = d->x; const prpe_view& y = d->y;
-  if (d->mid != MID || x.c != CIO || y.c != CIO || x.n != y.n || x.h != y.h || x.w != y.w) return PRPE_EINVAL;
+  const bool proj = x.c == MID;                          // projection block (layer1.0)
+  if (d->mid != MID || (x.c != CIO && !proj) || y.c != CIO || x.n != y.n || x.h != y.h || x.w != y.w)
+    return PRPE_EINVAL;
   if (x.sc != 1 || y.sc != 1 || x.sw % 4 || x.sh % 4 || x.sn % 4 || (uintptr_t)x.ptr % 16 || x.sw < 0 || x.sh < 0 ||
       y.sw % 4 || y.sh % 4 || y.sn % 4 || (uintptr_t)y.ptr % 16 || y.sw < 0 || y.sh < 0)
     return PRPE_EINVAL;
-  const int kneed[3] = {CIO, 9 * MID, MID};
+  const int kneed[3] = {(int)x.c, 9 * MID, proj ? 2 * MID : MID};
   for (int l = 0; l < 3; ++l) {
     if (!d->w_h16[l] || !d->w_l16[l] || !d->scale16[l] || !d->bias[l] || d->k_pad[l] != kneed[l]) return PRPE_EINVAL;
     if ((uintptr_t)d->w_h16[l] % 16 || (uintptr_t)d->w_l16[l] % 16 || (uintptr_t)d->scale16[l] % 16 ||
         (uintptr_t)d->bias[l] % 16)
       return PRPE_EINVAL;
   }
-  if (((int64_t)(x.h - 1) * x.sh + (int64_t)(x.w - 1) * x.sw + CIO) * 4 >= (1LL << 31) ||
+  if (((int64_t)(x.h - 1) * x.sh + (int64_t)(x.w - 1) * x.sw + x.c) * 4 >= (1LL << 31) ||
       ((int64_t)(y.h - 1) * y.sh + (int64_t)(y.w - 1) * y.sw + CIO) * 4 >= (1LL << 31))
     return PRPE_EINVAL;
   BneckK kp{};
   kp.x = x.ptr; kp.xsn = x.sn; kp.xsh = x.sh; kp.xsw = x.sw; kp.x_amax = d->x_amax;
   kp.y = y.ptr; kp.ysn = y.sn; kp.ysh = y.sh; kp.ysw = y.sw; kp.y_amax = d->y_amax;
   kp.N = x.n; kp.H = x.h; kp.W = x.w;
+  kp.proj = proj ? 1 : 0;
   for (int l = 0; l < 3; ++l) {
     kp.wh[l] = d->w_h16[l]; kp.wl[l] = d->w_l16[l]; kp.kp[l] = d->k_pad[l];
     kp.sc[l] = d->scale16[l]; kp.bi[l] = d->bias[l];

@@ -50,8 +50,10 @@ SMALLCO_TAPS = os.environ.get("PRPE_SMALLCO_TAPS", "1") != "0"
 # never reaches HBM. PRPE_TAPS_FUSE=0 runs the two convs separately.
 TAPS_FUSE = os.environ.get("PRPE_TAPS_FUSE", "1") != "0"
 # ResNet-50 layer1 identity blocks (1.1, 1.2) as ONE fused launch each (prpe_bottleneck: t1 / t2
-# only in LDS). PRPE_BNECK_FUSE=0 runs the three convs separately.
+# only in LDS). PRPE_BNECK_FUSE=0 runs the three convs separately. Block 1.0 (conv3 + the
+# downsample projection as one dual GEMM) likewise; PRPE_BNECK_PROJ=0 keeps it unfused.
 BNECK_FUSE = os.environ.get("PRPE_BNECK_FUSE", "1") != "0"
+BNECK_PROJ = os.environ.get("PRPE_BNECK_PROJ", "1") != "0"
 
 
 class _Prec:
@@ -336,6 +338,9 @@ class Engine:
                 if b > 0 and self._bneck_ok(x, planes):
                     x = self.bottleneck(q, x)
                     continue
+                if b == 0 and s == 1 and self._bneck_ok(x, planes, proj=True):
+                    x = self.bottleneck(q, x, proj=True)
+                    continue
                 o = self.conv(x, self.pk(q + ".conv1", q + ".conv1.weight", bn=q + ".bn1", act="relu"))
                 o = self.conv(o, self.pk(q + ".conv2", q + ".conv2.weight", s, 1, bn=q + ".bn2", act="relu"))
                 if b == 0:
@@ -348,17 +353,20 @@ class Engine:
                                   res=x, res_mode=RES_PRE)
         return x
 
-    def _bneck_ok(self, x, planes):
-        return (BNECK_FUSE and self.precision == 3 and planes == 64 and x.shape[3] == 4 * planes and
+    def _bneck_ok(self, x, planes, proj=False):
+        return (BNECK_FUSE and (BNECK_PROJ or not proj) and self.precision == 3 and planes == 64 and
+                x.shape[3] == (planes if proj else 4 * planes) and
                 x.is_contiguous() and getattr(x, "_prpe_amax", None) is not None)
 
-    def bottleneck(self, q, x):
-        """Identity-shortcut bottleneck ``q`` (torchvision Bottleneck.forward) as one fused launch
-        (prpe_bottleneck); same packs as the unfused path."""
+    def bottleneck(self, q, x, proj=False):
+        """Bottleneck ``q`` (torchvision Bottleneck.forward) as one fused launch (prpe_bottleneck);
+        same packs as the unfused path. ``proj``: block 0 of layer1 (stride 1, 64 -> 256 channels),
+        whose conv3 + downsample projection run as the dual GEMM of ``pk_dual``."""
         packs = (self.pk(q + ".conv1", q + ".conv1.weight", bn=q + ".bn1", act="relu"),
                  self.pk(q + ".conv2", q + ".conv2.weight", 1, 1, bn=q + ".bn2", act="relu"),
+                 self.pk_dual(q) if proj else
                  self.pk(q + ".conv3", q + ".conv3.weight", bn=q + ".bn3", act="relu"))
-        y = self.empty(*x.shape)
+        y = self.empty(*x.shape[:3], packs[2].co)
         ya = self.amax_slot(x.shape[0])
         if q in self.watch:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

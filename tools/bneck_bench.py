@@ -1,7 +1,8 @@
 """Micro-bench (GPU box): the fused identity bottleneck (prpe_bottleneck) vs the three unfused
-precision-3 launches on the layer1 shape [B, 160, 160, 256], random post-ReLU input.
+precision-3 launches on the layer1 shape [B, 160, 160, 256], random post-ReLU input; with
+--proj the projection block (layer1.0: x [B, 160, 160, 64], conv3 + downsample as one dual GEMM).
 
-    python tools/bneck_bench.py --batch 256 --iters 10 [--fused-only]
+    python tools/bneck_bench.py --batch 256 --iters 10 [--fused-only] [--proj]
 """
 import argparse
 import os
@@ -22,16 +23,19 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--fused-only", action="store_true")
+    ap.add_argument("--proj", action="store_true")
     a = ap.parse_args()
-    from test_gpu_bneck import _packs, _unfused  # noqa: E402
-    _, _, packs = _packs(400)
+    from test_gpu_bneck import _packs, _packs_proj, _unfused, _unfused_proj  # noqa: E402
+    _, _, packs = _packs_proj(500) if a.proj else _packs(400)
+    unfused = _unfused_proj if a.proj else _unfused
+    cin = 64 if a.proj else 256
     g = torch.Generator(DEV).manual_seed(1)
-    x = torch.relu(torch.randn(a.batch, 160, 160, 256, generator=g, device=DEV))
+    x = torch.relu(torch.randn(a.batch, 160, 160, cin, generator=g, device=DEV))
     xa = x.abs().flatten(1).amax(1).contiguous()
-    y = torch.empty_like(x)
+    y = torch.empty(a.batch, 160, 160, 256, device=DEV)
     ya = torch.zeros(a.batch, device=DEV)
     px = a.batch * 160 * 160
-    gb = 2 * px * 256 * 4 / 1e9                    # algorithmic: x read once, y written once
+    gb = px * (cin + 256) * 4 / 1e9                # algorithmic: x read once, y written once
 
     def timed(fn):
         fn()
@@ -45,9 +49,9 @@ def main():
         return e0.elapsed_time(e1) / a.iters
 
     ms = timed(lambda: ops.bottleneck(x, packs, y, xa, ya))
-    print(f"fused   bs={a.batch}: {ms:.3f} ms  {gb / ms:.2f} TB/s algorithmic ({gb:.2f} GB)", flush=True)
+    print(f"{'proj ' if a.proj else ''}fused   bs={a.batch}: {ms:.3f} ms  {gb / ms:.2f} TB/s algorithmic ({gb:.2f} GB)", flush=True)
     if not a.fused_only:
-        ms_u = timed(lambda: _unfused(x, xa, packs))
+        ms_u = timed(lambda: unfused(x, xa, packs))
         print(f"unfused bs={a.batch}: {ms_u:.3f} ms (three launches)", flush=True)
 
 
