@@ -153,12 +153,19 @@ int prpe_conv2d(const prpe_conv_desc* d, void* stream);
  * Fused ResNet bottleneck with identity shortcut, precision 3 (torchvision Bottleneck.forward,
  * v1.5; the reference trunk's layer1 blocks 1-2, modify_models.py:413-446):
  *   y = relu(bn3(conv3(relu(bn2(conv2_3x3(relu(bn1(conv1(x)))))))) + x)
- * x, y: [N, H, W, 4*mid] channel-contiguous (x 16-B aligned rows); x_amax [N] per-frame max|x|
+ * x, y: [N, H, W, 4*mid] channel-contiguous (x 16-B aligned rows; x [N, H, W, mid] for the
+ * projection block below); x_amax [N] per-frame max|x|
  * (as prpe_conv2d precision 3); y_amax (optional) raised to max|y[n]|. Weights as prpe_conv2d's
  * precision-3 packs: fp16 planes w_h16 / w_l16 [co_pad][k_pad] (conv1 k = 4 mid, conv2 chunk-major
  * k = 9 mid, conv3 k = mid), scale16 (the planes' 2^-e folded in) and bias [Co]. The two inner
  * activations never reach HBM; they are rounded to fp16 planes with one power-of-2 scale per
  * 8 x 16 output tile (per frame and tile: frames stay independent). mid = 64 (layer1).
+ * Projection block (layer1.0, stride 1): x has mid channels (x.c == mid, y.c == 4 mid) and
+ *   y = relu(bn3(conv3(t2)) + bn_d(downsample(x)))
+ * with conv3 and the downsample 1x1 as ONE dual GEMM over [t2 | x]: weight slot 2 is then the
+ * [4 mid][2 mid] matrix [s3 W3 | sd Wd] (both BN scales folded into its rows, k_pad = 2 mid) and
+ * bias[2] = b3 + bd; t2 and x share one power-of-2 scale (max of the tile's max|t2| and the
+ * frame's max|x|), as prpe_conv2d's dual-input GEMM.
  * x, y, the weight planes, scale16 and bias 16-B aligned, x / y pixel strides multiples of 4
  * floats, one frame of x and of y < 2^31 bytes; anything else returns -EINVAL.
  */

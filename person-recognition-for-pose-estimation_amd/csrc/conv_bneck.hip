@@ -46,40 +46,50 @@ struct BneckK {
   int kp[3];
   const float* sc[3]; const float* bi[3];
   int tiles_w, tiles_h, nwg;
-  int proj;                                              // x has MID channels (layer1.0, see BShape)
+  int mid;                                               // 64 or 128 (BShape)
+  int proj;                                              // x has mid channels (layer1.0, see BShape)
 };
 
 namespace {
 
 constexpr int BK_ = 32;
-constexpr int MID = 64, CIO = 256, TR = 8, TC = 16, NW = 8;     // CIO: output channels (and the
-                                                                 // identity block's input)
+constexpr int TR = 8, TC = 16, NW = 8;
 constexpr int HW_ = TC + 2, HP = (TR + 2) * HW_;        // 18, 180 haloed pixels
 constexpr int NRB1 = (HP + 15) / 16;                     // 12 row blocks of haloed pixels
 constexpr int CHB1 = NRB1 * 16 * 128;                    // bytes of one 32-channel chunk of t1
 constexpr int CHB2 = TR * TC * 128;                      // ... of t2
-constexpr int TT_BYTES = (MID / 32) * CHB1;              // 48 KB
-constexpr int STAGE = 2 * MID * 64;                      // one K-step of W1 / W2 (both planes)
-constexpr int RING_OFF = TT_BYTES;
-constexpr int W3_OFF = (MID / 32) * CHB2;                // 32 KB: after t2
 constexpr int W3_PART = 32 * 1024;                       // one W3 part (below) in the overlay
 constexpr int RING = 4;                                  // W1 / W2 ring stages (3 K-steps of lookahead)
-constexpr int LDS_BYTES = TT_BYTES + RING * STAGE;       // 80 KB: two workgroups per CU
-static_assert(W3_OFF + W3_PART <= RING_OFF + 2 * STAGE, "W3 part overlay below ring stage 2");
 
-// Block shape. Identity (layer1.1 / 1.2): x has CIO channels and is the residual; conv3 (K =
-// MID) runs in two parts of 128 output columns. Projection (PROJ, layer1.0): x has MID channels,
-// conv3 and the downsample projection are one dual GEMM over [t2 | x] (the engine's pk_dual pack,
-// K = 2 MID, W' = [s3 W3 | sd Wd]), run in four parts of 64 columns; no residual read.
-template <bool PROJ> struct BShape {
+// Block shape. MID = the inner width (64: layer1, 128: layer2), CIO = 4 MID output channels.
+// Identity (layer1.1-2, layer2.1-3): x has CIO channels and is the residual; conv3 (K = MID)
+// runs in parts of R3 output columns. Projection (PROJ, layer1.0): x has MID channels, conv3 and
+// the downsample projection are one dual GEMM over [t2 | x] (the engine's pk_dual pack, K = 2 MID,
+// W' = [s3 W3 | sd Wd]), run in four parts of 64 columns; no residual read.
+// LDS: TT (t1, then t2 in its first (MID/32) CHB2 bytes), then the W1 / W2 ring; a W3 part
+// overlays TT past t2 (and, at MID 64, ring stages 0-1). MID 64: 48 + 32 = 80 KB, two
+// workgroups per CU; MID 128: 96 + 64 = 160 KB, one.
+template <int MIDT, bool PROJ> struct BShape {
+  static constexpr int MID = MIDT, CIO = 4 * MIDT;
   static constexpr int CIN = PROJ ? MID : CIO;           // x channels
   static constexpr int NK1 = CIN / BK_;                  // phase-1 K-steps
   static constexpr int NKS3 = PROJ ? 2 * MID / BK_ : MID / BK_;   // phase-3 K-steps
-  static constexpr int R3 = PROJ ? 64 : 128;             // output columns per phase-3 part
+  static constexpr int R3 = PROJ || MID > 64 ? 64 : 128; // output columns per phase-3 part
   static constexpr int NPART = CIO / R3;
   static constexpr int W3_STEP = 2 * R3 * 64;            // one K-step of a part (both planes)
+  static constexpr int TT_BYTES = (MID / 32) * CHB1;
+  static constexpr int STAGE = 2 * MID * 64;             // one K-step of W1 / W2 (both planes)
+  static constexpr int PPW = STAGE / 1024 / NW;          // its LDS-DMA pieces per wave
+  static constexpr int RING_OFF = TT_BYTES;
+  static constexpr int W3_OFF = (MID / 32) * CHB2;       // after t2
+  static constexpr int LDS_BYTES = TT_BYTES + RING * STAGE;
+  static constexpr int WPC = LDS_BYTES <= 80 * 1024 ? 2 : 1;   // workgroups per CU
+  static_assert(!PROJ || MID == 64, "projection block: layer1.0 only");
+  static_assert(PPW >= 1 && STAGE == PPW * NW * 1024, "W ring pieces");
   static_assert(NKS3 * W3_STEP == W3_PART, "W3 part size");
   static_assert(NKS3 * 2 * (R3 / 16) == 4 * NW, "4 W3 pieces per wave and part");
+  static_assert(W3_OFF + W3_PART <= RING_OFF + 2 * STAGE, "W3 part overlay below ring stage 2");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
@@ -116,11 +126,13 @@ __device__ __forceinline__ f32x4 mfma3t(const f16x8 (&w)[2], const f16x8 (&a)[2]
   return c;
 }
 
-template <bool PROJ>
-__global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
-  using S = BShape<PROJ>;
-  constexpr int CIN = S::CIN, NK1 = S::NK1, R3 = S::R3, W3_STEP = S::W3_STEP;
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
+template <int MIDT, bool PROJ>
+__global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kernel(BneckK p) {
+  using S = BShape<MIDT, PROJ>;
+  constexpr int MID = S::MID, CIO = S::CIO, CIN = S::CIN, NK1 = S::NK1, R3 = S::R3, W3_STEP = S::W3_STEP;
+  constexpr int STAGE = S::STAGE, PPW = S::PPW, RING_OFF = S::RING_OFF, W3_OFF = S::W3_OFF;
+  constexpr int NJ1 = MID / 16;                              // 16-channel column blocks of t1 / t2
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[S::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fg = lane >> 4;
   int L = xcd_remap(blockIdx.x, p.nwg);
@@ -141,14 +153,26 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
     wr[l][0] = buf_rsrc(p.wh[l], rows * p.kp[l] * 2);
     wr[l][1] = buf_rsrc(p.wl[l], rows * p.kp[l] * 2);
   }
-  // W1 / W2 ring piece of this wave: plane wave / 4, rows 16 (wave % 4) .. +16
-  const int bq = wave >> 2, brb = wave & 3;
-  const int bnrow = brb * 16 + (lane >> 2);
-  const int bch = (lane & 3) ^ swzF(bnrow);
-  const int bdst = RING_OFF + (bq * MID + brb * 16) * 64;
+  // W1 / W2 ring pieces of this wave: piece j = wave PPW + i -> plane j / NJ1 (= the wave's
+  // plane: waves 0-3 the hi plane, 4-7 the lo), rows 16 (j % NJ1) .. +16. The plane's descriptors
+  // are selected once (wave-uniform SGPRs: a per-piece select spilled them to scratch)
+  static_assert(NJ1 % PPW == 0 && PPW * NW == 2 * NJ1, "W ring piece map");
+  const bool bq = wave * PPW / NJ1 != 0;
+  const __amdgpu_buffer_rsrc_t wq0 = bq ? wr[0][1] : wr[0][0], wq1 = bq ? wr[1][1] : wr[1][0];
+  int bnrow[PPW], bch[PPW], bdst[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int j = wave * PPW + i;
+    bnrow[i] = (j % NJ1) * 16 + (lane >> 2);
+    bch[i] = (lane & 3) ^ swzF(bnrow[i]);
+    bdst[i] = RING_OFF + ((j / NJ1) * MID + (j % NJ1) * 16) * 64;
+  }
   auto issue_w = [&](int l, int kt, int stage) {           // l = 0 (W1) or 1 (W2)
-    const unsigned vo = (unsigned)((bnrow * p.kp[l] + bch * 8) * 2);
-    bl_lds16(bq ? wr[l][1] : wr[l][0], lds + bdst + stage * STAGE, vo, kt * BK_ * 2);
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const unsigned vo = (unsigned)((bnrow[i] * p.kp[l] + bch[i] * 8) * 2);
+      bl_lds16(l ? wq1 : wq0, lds + bdst[i] + stage * STAGE, vo, kt * BK_ * 2);
+    }
   };
   // the W stream: steps u < NK1 are W1's K-steps, the next 18 W2's; step u goes to stage u % RING
   constexpr int NK2 = (MID / 32) * 9, NU = NK1 + NK2;
@@ -174,11 +198,11 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
     pv[i] = px < HP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && rb < NRB1;
     av[i] = pv[i] ? (unsigned)(((int64_t)ih * p.xsh + (int64_t)iw * p.xsw + fg * 8) * 4) : BL_OOB;
   }
-  f32x4 acc1[2][4];
+  f32x4 acc1[2][NJ1];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ1; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // A straight from global into registers, two K-steps ahead (raw[step & 1])
   f4 raw[2][2][2];
   auto load_a = [&](int kt) {
@@ -204,8 +228,9 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
     }
   };
   // Per step kt: [wait + barrier] W(kt + RING - 1), A(kt + 2) issued, MFMAs on A(kt), split of
-  // A(kt + 1). The wait leaves in flight exactly the ops issued after this wave's piece of
-  // W(kt) (counted per step below: na = A loads per step), so A stays two steps ahead.
+  // A(kt + 1). The wait leaves in flight exactly the ops issued after this wave's pieces of
+  // W(kt) (counted per step below: PPW pieces per W step, na = A loads per step), so A stays two
+  // steps ahead.
   static_assert(RING == 4 && NK1 >= 2, "phase-1 wait counts");
 #pragma unroll
   for (int u = 0; u < RING - 1; ++u) issue_wu(u);
@@ -217,15 +242,15 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
     // ops issued after W(kt): kt = 0: W1, W2, A0, A1; middle steps: 2 W + 3 A steps (fewer only
     // where the count is not needed: W(1), W(2) precede A(0)); last: 2 W + 2 A steps
     if (two) {
-      if (kt == 0 || kt == NK1 - 1) wait_barrier<2 + 2 * 4>(); else wait_barrier<2 + 3 * 4>();
+      if (kt == 0 || kt == NK1 - 1) wait_barrier<2 * PPW + 2 * 4>(); else wait_barrier<2 * PPW + 3 * 4>();
     } else {
-      if (kt == 0 || kt == NK1 - 1) wait_barrier<2 + 2 * 2>(); else wait_barrier<2 + 3 * 2>();
+      if (kt == 0 || kt == NK1 - 1) wait_barrier<2 * PPW + 2 * 2>(); else wait_barrier<2 * PPW + 3 * 2>();
     }
     issue_wu(kt + RING - 1);
     if (kt + 2 < NK1) load_a(kt + 2);
     const unsigned char* sb = lds + RING_OFF + (kt % RING) * STAGE;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ1; ++j) {
       f16x8 b[2];
       b_frags(sb, MID, j, fr, fg, b);
       acc1[0][j] = mfma3t(b, af[0], acc1[0][j]);
@@ -237,7 +262,7 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   // Lane (fr, fg) holds channels j*16 + fg*4 .. +3 of pixel rb*16 + fr.
   float m1 = 0.f;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NJ1; ++j) {
     const int c0 = j * 16 + fg * 4;
     const f4 s = *reinterpret_cast<const f4*>(p.sc[0] + c0), b = *reinterpret_cast<const f4*>(p.bi[0] + c0);
 #pragma unroll
@@ -267,7 +292,7 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   for (int i = 0; i < 2; ++i) {
     if (i == 1 && !two) continue;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NJ1; ++j) {
       unsigned long long pl[2];
       split_planes_f16(acc1[i][j], s1, pl);
       put_planes4(lds, CHB1, (wave + i * NW) * 16 + fr, j * 16 + fg * 4, pl);
@@ -282,10 +307,10 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
     const int px = (wave + t / 3) * HW_ + fr + t % 3;
     aoff[t] = px * 128 + (((2 * fg) ^ ((px >> 1) & 7)) << 4);
   }
-  f32x4 acc2[4];
+  f32x4 acc2[NJ1];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  static_assert(MID / 32 == 2 && RING == 4, "phase-2 wait counts");
+  for (int j = 0; j < NJ1; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  static_assert(RING == 4, "phase-2 wait counts");
   int u = NK1;
 #pragma unroll 1
   for (int c = 0; c < MID / 32; ++c) {
@@ -293,15 +318,15 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
 #pragma unroll
     for (int t = 0; t < 9; ++t, ++u) {
       // W stream step u (its first RING - 1 were issued during phase 1): in flight after this
-      // wave's piece of W(u) are W(u+1), W(u+2) -- fewer in the last two steps
-      if (c == 1 && t >= 7) wait_barrier<0>(); else wait_barrier<RING - 2>();
+      // wave's pieces of W(u) are those of W(u+1), W(u+2) -- fewer in the last two steps
+      if (c == MID / 32 - 1 && t >= 7) wait_barrier<0>(); else wait_barrier<(RING - 2) * PPW>();
       issue_wu(u + RING - 1);
       f16x8 a[2];
       a[0] = *reinterpret_cast<const f16x8*>(tc + aoff[t]);
       a[1] = *reinterpret_cast<const f16x8*>(tc + (aoff[t] ^ 16));
       const unsigned char* sb = lds + RING_OFF + (u % RING) * STAGE;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < NJ1; ++j) {
         f16x8 b[2];
         b_frags(sb, MID, j, fr, fg, b);
         acc2[j] = mfma3t(b, a, acc2[j]);
@@ -314,7 +339,7 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   const bool ov = oy < p.H && ox < p.W;
   float m2 = 0.f;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NJ1; ++j) {
     const int c0 = j * 16 + fg * 4;
     const f4 s = *reinterpret_cast<const f4*>(p.sc[1] + c0), b = *reinterpret_cast<const f4*>(p.bi[1] + c0);
 #pragma unroll
@@ -366,7 +391,7 @@ __global__ __launch_bounds__(NW * 64, 2) void bneck_kernel(BneckK p) {
   const int e2 = f16_scale_exp(PROJ ? fmaxf(m2, am) : m2);
   const float s2 = ldexpf(1.f, 15 - e2), inv2 = ldexpf(1.f, e2 - 15);
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NJ1; ++j) {
     unsigned long long pl[2];
     split_planes_f16(acc2[j], s2, pl);
     put_planes4(lds, CHB2, wave * 16 + fr, j * 16 + fg * 4, pl);
@@ -473,8 +498,9 @@ int bneck_launch(const BneckK& kp0, hipStream_t st) {
   const int64_t nwg = (int64_t)kp.N * kp.tiles_w * kp.tiles_h;
   if (nwg <= 0 || nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
-  if (kp.proj) hipLaunchKernelGGL(bneck_kernel<true>, dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
-  else hipLaunchKernelGGL(bneck_kernel<false>, dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  if (kp.proj) hipLaunchKernelGGL((bneck_kernel<64, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  else if (kp.mid == 64) hipLaunchKernelGGL((bneck_kernel<64, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  else hipLaunchKernelGGL((bneck_kernel<128, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
   return launch_status();
 }
 
@@ -484,8 +510,10 @@ extern "C" int prpe_bottleneck(const prpe_bneck_desc* d, void* stream) {
   using namespace prpe_k;
   if (!d || !view_ok(&d->x) || !view_ok(&d->y) || !d->x_amax) return PRPE_EINVAL;
   const prpe_view& x = d->x; const prpe_view& y = d->y;
+  const int MID = d->mid, CIO = 4 * d->mid;
   const bool proj = x.c == MID;                          // projection block (layer1.0)
-  if (d->mid != MID || (x.c != CIO && !proj) || y.c != CIO || x.n != y.n || x.h != y.h || x.w != y.w)
+  if ((MID != 64 && MID != 128) || (proj && MID != 64) || (x.c != CIO && !proj) || y.c != CIO || x.n != y.n ||
+      x.h != y.h || x.w != y.w)
     return PRPE_EINVAL;
   if (x.sc != 1 || y.sc != 1 || x.sw % 4 || x.sh % 4 || x.sn % 4 || (uintptr_t)x.ptr % 16 || x.sw < 0 || x.sh < 0 ||
       y.sw % 4 || y.sh % 4 || y.sn % 4 || (uintptr_t)y.ptr % 16 || y.sw < 0 || y.sh < 0)
@@ -505,6 +533,7 @@ extern "C" int prpe_bottleneck(const prpe_bneck_desc* d, void* stream) {
   kp.y = y.ptr; kp.ysn = y.sn; kp.ysh = y.sh; kp.ysw = y.sw; kp.y_amax = d->y_amax;
   kp.N = x.n; kp.H = x.h; kp.W = x.w;
   kp.proj = proj ? 1 : 0;
+  kp.mid = MID;
   for (int l = 0; l < 3; ++l) {
     kp.wh[l] = d->w_h16[l]; kp.wl[l] = d->w_l16[l]; kp.kp[l] = d->k_pad[l];
     kp.sc[l] = d->scale16[l]; kp.bi[l] = d->bias[l];

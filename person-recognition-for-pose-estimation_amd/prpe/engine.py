@@ -49,11 +49,14 @@ SMALLCO_TAPS = os.environ.get("PRPE_SMALLCO_TAPS", "1") != "0"
 # .10), the tap GEMM runs in the producer's epilogue (prpe_conv_desc.w2): the 128-channel map
 # never reaches HBM. PRPE_TAPS_FUSE=0 runs the two convs separately.
 TAPS_FUSE = os.environ.get("PRPE_TAPS_FUSE", "1") != "0"
-# ResNet-50 layer1 identity blocks (1.1, 1.2) as ONE fused launch each (prpe_bottleneck: t1 / t2
+# ResNet-50 identity blocks (1.1, 1.2) as ONE fused launch each (prpe_bottleneck: t1 / t2
 # only in LDS). PRPE_BNECK_FUSE=0 runs the three convs separately. Block 1.0 (conv3 + the
 # downsample projection as one dual GEMM) likewise; PRPE_BNECK_PROJ=0 keeps it unfused.
 BNECK_FUSE = os.environ.get("PRPE_BNECK_FUSE", "1") != "0"
 BNECK_PROJ = os.environ.get("PRPE_BNECK_PROJ", "1") != "0"
+# ... and layer2's identity blocks (2.1-2.3, inner width 128, one 160-KB workgroup per CU);
+# PRPE_BNECK_L2=0 keeps them unfused
+BNECK_L2 = os.environ.get("PRPE_BNECK_L2", "1") != "0"
 
 
 class _Prec:
@@ -354,7 +357,8 @@ class Engine:
         return x
 
     def _bneck_ok(self, x, planes, proj=False):
-        return (BNECK_FUSE and (BNECK_PROJ or not proj) and self.precision == 3 and planes == 64 and
+        return (BNECK_FUSE and (BNECK_PROJ or not proj) and self.precision == 3 and
+                (planes == 64 or (planes == 128 and BNECK_L2 and not proj)) and
                 x.shape[3] == (planes if proj else 4 * planes) and
                 x.is_contiguous() and getattr(x, "_prpe_amax", None) is not None)
 

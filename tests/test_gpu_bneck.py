@@ -200,3 +200,68 @@ def test_bottleneck_proj_rejects_wrong_dual_pack():
     with pytest.raises(PrpeError):                        # conv3 pack without the projection half
         ops.bottleneck(x, (packs[0], packs[1], ident[2]), torch.empty(1, 8, 8, 256, device=DEV),
                        torch.ones(1, device=DEV))
+
+
+# ---------------------------------------------------------------- layer2 identity blocks (mid 128)
+def _packs128(seed):
+    w1 = rnd(128, 512, 1, 1, seed=seed, scale=1.0 / 22)
+    w2 = rnd(128, 128, 3, 3, seed=seed + 1, scale=1.0 / 34)
+    w3 = rnd(512, 128, 1, 1, seed=seed + 2, scale=1.0 / 11)
+    bn = [(torch.rand(c, generator=_g(seed + 10 + i)) + 0.5, rnd(c, seed=seed + 20 + i, scale=0.3))
+          for i, c in enumerate((128, 128, 512))]
+    bn[2] = (bn[2][0] * 0.2, bn[2][1])
+    p1 = pack.pack_conv("c1", w1, 1, 0, DEV, scale=bn[0][0], bias=bn[0][1], act="relu")
+    p2 = pack.pack_conv("c2", w2, 1, 1, DEV, scale=bn[1][0], bias=bn[1][1], act="relu")
+    p3 = pack.pack_conv("c3", w3, 1, 0, DEV, scale=bn[2][0], bias=bn[2][1], act="relu")
+    return (w1, w2, w3), bn, (p1, p2, p3)
+
+
+def _unfused128(x, xa, packs):
+    N, H, W, _ = x.shape
+    t1 = torch.empty(N, H, W, 128, device=DEV)
+    t2 = torch.empty(N, H, W, 128, device=DEV)
+    y = torch.empty(N, H, W, 512, device=DEV)
+    a1, a2 = torch.zeros(N, device=DEV), torch.zeros(N, device=DEV)
+    ops.conv2d(x, packs[0], t1, precision=3, x_amax=xa, y_amax=a1)
+    ops.conv2d(t1, packs[1], t2, precision=3, x_amax=a1, y_amax=a2)
+    ops.conv2d(t2, packs[2], y, res=x, res_mode=RES_PRE, precision=3, x_amax=a2)
+    return y
+
+
+@pytest.mark.parametrize("N,H,W", [(2, 20, 20), (1, 24, 40), (3, 17, 9), (2, 80, 80)])
+def test_bottleneck128_fused_vs_fp64_and_unfused(N, H, W):
+    ws, bn, packs = _packs128(600)
+    g = torch.Generator(DEV).manual_seed(N * 1000 + H + 2)
+    x = torch.relu(torch.randn(N, H, W, 512, generator=g, device=DEV)) * 2.0
+    xa = x.abs().flatten(1).amax(1).contiguous()
+    y = torch.empty_like(x)
+    ya = torch.zeros(N, device=DEV)
+    ops.bottleneck(x, packs, y, xa, ya)
+    yu = _unfused128(x, xa, packs)
+    torch.cuda.synchronize()
+    ref = _ref64(x.cpu(), ws, bn)
+    e_f = (y.cpu().double() - ref).abs().max().item()
+    e_u = (yu.cpu().double() - ref).abs().max().item()
+    scale = ref.abs().max().item()
+    print(f"bneck128 {N}x{H}x{W}: fused {e_f:.2e} unfused {e_u:.2e} max|y| {scale:.2f}")
+    assert e_f <= 3 * e_u + 2 ** -22 * scale, (e_f, e_u)
+    assert torch.isfinite(y).all()
+    assert torch.equal(ya.cpu(), y.abs().flatten(1).amax(1).cpu())
+
+
+def test_bottleneck128_frames_independent_and_deterministic():
+    _, _, packs = _packs128(610)
+    g = torch.Generator(DEV).manual_seed(11)
+    x = torch.relu(torch.randn(96, 80, 80, 512, generator=g, device=DEV))
+    x[2] *= 50.0
+    xa = x.abs().flatten(1).amax(1).contiguous()
+    ys = []
+    for _ in range(2):
+        y = torch.empty_like(x)
+        ops.bottleneck(x, packs, y, xa)
+        ys.append(y)
+    y1 = torch.empty_like(x[1:2])
+    ops.bottleneck(x[1:2].contiguous(), packs, y1, xa[1:2].contiguous())
+    torch.cuda.synchronize()
+    assert torch.equal(ys[0], ys[1])
+    assert torch.equal(ys[0][1:2], y1)
