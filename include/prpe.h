@@ -159,7 +159,8 @@ int prpe_conv2d(const prpe_conv_desc* d, void* stream);
  * precision-3 packs: fp16 planes w_h16 / w_l16 [co_pad][k_pad] (conv1 k = 4 mid, conv2 chunk-major
  * k = 9 mid, conv3 k = mid), scale16 (the planes' 2^-e folded in) and bias [Co]. The two inner
  * activations never reach HBM; they are rounded to fp16 planes with one power-of-2 scale per
- * 8 x 16 output tile (per frame and tile: frames stay independent). mid = 64 (layer1).
+ * 8 x 16 output tile (per frame and tile: frames stay independent). mid = 64 (layer1) or 128
+ * (layer2, identity blocks only).
  * Projection block (layer1.0, stride 1): x has mid channels (x.c == mid, y.c == 4 mid) and
  *   y = relu(bn3(conv3(t2)) + bn_d(downsample(x)))
  * with conv3 and the downsample 1x1 as ONE dual GEMM over [t2 | x]: weight slot 2 is then the

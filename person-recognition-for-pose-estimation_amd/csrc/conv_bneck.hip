@@ -84,6 +84,9 @@ template <int MIDT, bool PROJ> struct BShape {
   static constexpr int W3_OFF = (MID / 32) * CHB2;       // after t2
   static constexpr int LDS_BYTES = TT_BYTES + RING * STAGE;
   static constexpr int WPC = LDS_BYTES <= 80 * 1024 ? 2 : 1;   // workgroups per CU
+  // two W3 part buffers when the free LDS of phase 3 holds them (MID 128: TT past t2 + ring
+  // stages 0-1): part h + 1 is then DMA'd under part h's MFMAs instead of after them
+  static constexpr bool W3DB = W3_OFF + 2 * W3_PART <= RING_OFF + 2 * STAGE;
   static_assert(!PROJ || MID == 64, "projection block: layer1.0 only");
   static_assert(PPW >= 1 && STAGE == PPW * NW * 1024, "W ring pieces");
   static_assert(NKS3 * W3_STEP == W3_PART, "W3 part size");
@@ -367,9 +370,11 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
       xc[ks][1] = bl_f4(xr, cvo + 16, ks * BK_ * 4);
     }
   }
-  // W3 part h (R3 output columns, all NKS3 K-steps, both planes) into the overlay (TT's last
-  // 16 KB + ring stages 0-1): 32 pieces, 4 per wave
+  // W3 part h (R3 output columns, all NKS3 K-steps, both planes) into the overlay (TT past t2 +
+  // ring stages 0-1; buffer h & 1 when double-buffered): 32 pieces, 4 per wave
+  constexpr bool W3DB = S::W3DB;
   auto issue_w3 = [&](int h) {
+    unsigned char* const w3b = lds + W3_OFF + (W3DB ? (h & 1) * W3_PART : 0);
     constexpr int RB3 = R3 / 16;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -378,7 +383,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
       const int nrow = rb * 16 + (lane >> 2);
       const int ch = (lane & 3) ^ swzF(nrow);
       const unsigned vo = (unsigned)(((h * R3 + nrow) * p.kp[2] + ch * 8) * 2);
-      bl_lds16(q ? wr[2][1] : wr[2][0], lds + W3_OFF + ks * W3_STEP + (q * R3 + rb * 16) * 64, vo, ks * BK_ * 2);
+      bl_lds16(q ? wr[2][1] : wr[2][0], w3b + ks * W3_STEP + (q * R3 + rb * 16) * 64, vo, ks * BK_ * 2);
     }
   };
   issue_w3(0);
@@ -438,6 +443,11 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
       // W3 part h was issued before part h-1's NJ stores and this part's residual loads
       wait_barrier<NJ + NRES>();
     }
+    if constexpr (W3DB) {
+      // every wave is past part h-1's MFMAs: its buffer takes part h + 1 now
+      if (h + 1 < NPART) issue_w3(h + 1);
+      asm volatile("" ::: "memory");
+    }
     f32x4 acc3[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc3[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -451,7 +461,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
         a[0] = xb[ks - MID / BK_ < NXK ? ks - MID / BK_ : 0][0];
         a[1] = xb[ks - MID / BK_ < NXK ? ks - MID / BK_ : 0][1];
       }
-      const unsigned char* sb = lds + W3_OFF + ks * W3_STEP;
+      const unsigned char* sb = lds + W3_OFF + (W3DB ? (h & 1) * W3_PART : 0) + ks * W3_STEP;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         f16x8 b[2];
@@ -459,7 +469,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
         acc3[j] = mfma3t(b, a, acc3[j]);
       }
     }
-    if (h + 1 < NPART) {
+    if (!W3DB && h + 1 < NPART) {
       // every wave is done reading W3 part h (its ds_reads fed the MFMAs above): overwrite it
       // with part h + 1 now, BEFORE this part's stores
       __builtin_amdgcn_sched_barrier(0);
