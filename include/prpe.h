@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PRPE_ABI_VERSION 6
+#define PRPE_ABI_VERSION 7
 
 /* activations (epilogues/prologues) */
 enum prpe_act {
@@ -183,6 +183,35 @@ typedef struct prpe_bneck_desc {
   const float* bias[3];
 } prpe_bneck_desc;
 int prpe_bottleneck(const prpe_bneck_desc* d, void* stream);
+
+/*
+ * ResNet-50 stem + max-pool in one launch, precision 3 (torchvision resnet50 conv1 7x7/2 pad 3
+ * -> bn1 -> relu -> maxpool 3x3/2 pad 1; the reference trunk, modify_models.py:413-446):
+ *   y[n, py, px, c] = max over the 3x3 / 2 window of relu(bn1(conv1(x)))
+ * x: the frames as a zero-bordered NHWC4 buffer, element (n, h, w, c) at x + n*xsn + h*xsh + 4*w + c,
+ * h < H + 6, w < W + 8, the image at rows / columns 3 .. (prpe_copy_pad writes it; the 4th
+ * channel and the border are zero); x_amax [N] per-frame max|x|. The weight pack is the stem's
+ * precision-3 pack of prpe_conv2d's chunked form: W'[64][224], k = kh*32 + kw*4 + c (zero for
+ * kw = 7, c = 3), fp16 planes w_h16 / w_l16 with scale16 (2^-e folded in) and bias [64]. Every
+ * stem value equals prpe_conv2d's on the same view bit for bit; the stem map never reaches HBM.
+ * y: [N, H/4, W/4, 64], channel-contiguous, 16-B aligned; y_amax (optional) raised to max|y[n]|
+ * (= the stem map's max: every stem output lies in some window). H, W multiples of 4, one frame
+ * of x < 2^31 bytes; anything else returns -EINVAL.
+ */
+typedef struct prpe_stem_desc {
+  const float* x;
+  int64_t xsn, xsh;
+  int32_t n, h, w;
+  const float* x_amax;
+  const uint16_t* w_h16;
+  const uint16_t* w_l16;
+  int32_t k_pad;
+  const float* scale16;
+  const float* bias;
+  prpe_view y;
+  float* y_amax;
+} prpe_stem_desc;
+int prpe_stem_maxpool(const prpe_stem_desc* d, void* stream);
 
 /*
  * conv3x3(pad 1) o bilinear-upsample, second stage of the exact algebraic rewrite

@@ -14,7 +14,7 @@ from ._srchash import source_hash
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libprpe.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class PrpeError(RuntimeError):
@@ -50,6 +50,13 @@ class BneckDesc(C.Structure):
                 ("scale16", C.c_void_p * 3), ("bias", C.c_void_p * 3)]
 
 
+class StemDesc(C.Structure):
+    _fields_ = [("x", C.c_void_p), ("xsn", C.c_int64), ("xsh", C.c_int64), ("n", C.c_int32), ("h", C.c_int32),
+                ("w", C.c_int32), ("x_amax", C.c_void_p), ("w_h16", C.c_void_p), ("w_l16", C.c_void_p),
+                ("k_pad", C.c_int32), ("scale16", C.c_void_p), ("bias", C.c_void_p), ("y", View),
+                ("y_amax", C.c_void_p)]
+
+
 ACT = {"none": 0, "relu": 1, "silu": 2, "prelu": 3, "gelu": 4, "sigmoid": 5}
 RES_NONE, RES_PRE, RES_POST = 0, 1, 2
 
@@ -63,6 +70,7 @@ SIGNATURES = {
     "prpe_conv2d_workspace_bytes": (C.c_int64, [C.POINTER(ConvDesc)]),
     "prpe_conv2d": (C.c_int, [C.POINTER(ConvDesc), _P]),
     "prpe_bottleneck": (C.c_int, [C.POINTER(BneckDesc), _P]),
+    "prpe_stem_maxpool": (C.c_int, [C.POINTER(StemDesc), _P]),
     "prpe_upconv3x3_workspace_bytes": (C.c_int64, [_VP, _VP]),
     "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _I, _P, _L, _P]),
     "prpe_dwconv": (C.c_int, [_VP, _VP, _VP, _P, _I, _I, _I, _P, _P, _I, _P]),

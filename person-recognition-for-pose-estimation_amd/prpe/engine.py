@@ -57,6 +57,9 @@ BNECK_PROJ = os.environ.get("PRPE_BNECK_PROJ", "1") != "0"
 # ... and layer2's identity blocks (2.1-2.3, inner width 128, one 160-KB workgroup per CU);
 # PRPE_BNECK_L2=0 keeps them unfused
 BNECK_L2 = os.environ.get("PRPE_BNECK_L2", "1") != "0"
+# stem conv + max-pool as ONE launch (prpe_stem_maxpool: the [B, 320, 320, 64] stem map stays in
+# LDS); PRPE_STEM_POOL=0 runs prpe_conv2d + prpe_maxpool
+STEM_POOL = os.environ.get("PRPE_STEM_POOL", "1") != "0"
 
 
 class _Prec:
@@ -295,7 +298,7 @@ class Engine:
             return 3
         return None
 
-    def stem(self, x_nchw, flip_w=False):
+    def stem(self, x_nchw, flip_w=False, pool=False):
         """conv1 7x7/2 pad 3 + bn1 + relu (torchvision resnet50) as a channel-chunked conv.
 
         The NCHW frames are copied once into a zero-bordered NHWC4 buffer [B, H+6, W+8, 4]
@@ -326,14 +329,34 @@ class Engine:
             stem = pack_matrix("backbone.conv1", wv.reshape(w.shape[0], 7 * 32), 7, 1, 32, 2, 0, self.device,
                                scale=s, bias=b, act="relu", k_order=1)
             self._packs["backbone.conv1"] = stem
+        if pool and STEM_POOL and self.precision == 3 and H0 % 4 == 0 and W0 % 4 == 0:
+            # + maxpool 3x3/2 pad 1 in the same launch; max-pooling never raises max|x|, so the
+            # pooled map's slot is the stem map's maximum (what the unfused path hands on)
+            y = self.empty(B0, H0 // 4, W0 // 4, stem.co)
+            ya = self.amax_slot(B0)
+            name = "backbone.conv1+maxpool"
+            if name in self.watch:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ops.stem_maxpool(buf, H0, W0, amax, stem, y, ya)
+                e1.record()
+                self.events.setdefault(name, []).append((e0, e1, B0 * (H0 // 2) * (W0 // 2), stem, 3, buf.numel()))
+            else:
+                ops.stem_maxpool(buf, H0, W0, amax, stem, y, ya)
+            y._prpe_amax = ya
+            y._prpe_pooled = True
+            return y
         return self.conv(v, stem)
 
     def _trunk(self, x_nchw, flip_w=False):
-        y = self.stem(x_nchw, flip_w)
-        B, H, W, C = y.shape
-        mp = self.empty(B, (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1, C)
-        x = ops.maxpool(y, mp, 3, 2, 1)
-        x._prpe_amax = y._prpe_amax        # max-pooling never raises max|x|
+        y = self.stem(x_nchw, flip_w, pool=True)
+        if getattr(y, "_prpe_pooled", False):
+            x = y
+        else:
+            B, H, W, C = y.shape
+            mp = self.empty(B, (H + 2 - 3) // 2 + 1, (W + 2 - 3) // 2 + 1, C)
+            x = ops.maxpool(y, mp, 3, 2, 1)
+            x._prpe_amax = y._prpe_amax    # max-pooling never raises max|x|
         for li, (planes, blocks, stride) in enumerate(arch.RESNET50_STAGES, 1):
             for b in range(blocks):
                 q = f"backbone.layer{li}.{b}"

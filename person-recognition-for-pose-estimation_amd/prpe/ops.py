@@ -10,7 +10,7 @@ import ctypes as C
 
 import torch
 
-from ._lib import ACT, RES_NONE, BneckDesc, ConvDesc, PrpeError, View, check, lib
+from ._lib import ACT, RES_NONE, BneckDesc, ConvDesc, PrpeError, StemDesc, View, check, lib
 
 
 def _stream() -> C.c_void_p:
@@ -125,6 +125,27 @@ def bottleneck(x, packs, y, x_amax, y_amax=None):
         d.w_h16[i], d.w_l16[i], d.scale16[i], d.bias[i] = h16.data_ptr(), l16.data_ptr(), s16.data_ptr(), b.data_ptr()
         d.k_pad[i] = pk.k_pad
     check(lib().prpe_bottleneck(C.byref(d), _stream()), "prpe_bottleneck")
+    return y
+
+
+def stem_maxpool(buf, h, w, x_amax, pack, y, y_amax=None):
+    """ResNet-50 stem conv (7x7/2, BN, ReLU) + max-pool 3x3/2 in one launch (prpe_stem_maxpool,
+    include/prpe.h). ``buf``: the zero-bordered NHWC4 frames [N, h+6, w+8, 4] (Engine.stem's
+    buffer, image at rows / columns 3..); ``pack``: the stem's chunked precision-3 ConvPack
+    (k_pad 224); y [N, h/4, w/4, 64]."""
+    _gpu(buf, y, x_amax)
+    if not buf.is_contiguous() or buf.dim() != 4 or buf.shape[3] != 4:
+        raise PrpeError("stem_maxpool: buf must be a contiguous [N, H+6, W+8, 4] buffer")
+    d = StemDesc()
+    d.x, d.xsn, d.xsh = buf.data_ptr(), buf.stride(0), buf.stride(1)
+    d.n, d.h, d.w = buf.shape[0], h, w
+    d.x_amax = x_amax.data_ptr()
+    h16, l16, s16 = pack.f16_planes()
+    b = pack.bias if pack.bias is not None else torch.zeros(pack.co, device=buf.device)
+    d.w_h16, d.w_l16, d.k_pad, d.scale16, d.bias = h16.data_ptr(), l16.data_ptr(), pack.k_pad, s16.data_ptr(), b.data_ptr()
+    d.y = view(y)
+    d.y_amax = _ptr(y_amax)
+    check(lib().prpe_stem_maxpool(C.byref(d), _stream()), "prpe_stem_maxpool")
     return y
 
 

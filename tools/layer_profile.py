@@ -29,7 +29,7 @@ def main():
     x = synth.frames(a.batch).cuda()
     m.forward_all(x, face_stride=[8.0, 16.0, 32.0], concurrent=False)
     torch.cuda.synchronize()
-    e.watch = set(e._packs.keys())
+    e.watch = set(e._packs.keys()) | {"backbone.conv1+maxpool"}
     # fused bottlenecks (Engine.bottleneck) are timed under the block name; their row shows conv2
     e.watch |= {f"backbone.layer{li}.{b}" for li, (_, n, _) in enumerate(arch.RESNET50_STAGES, 1)
                 for b in range(n)}
