@@ -14,9 +14,9 @@
 // per-channel-scaled fp16 weight planes, three MFMA terms smallest first) and the same epilogue
 // arithmetic, so every stem value equals prpe_conv2d's bit for bit (tested).
 //
-// One workgroup = one frame x one strip of 32 pooled columns (65 stem columns), walking the
-// frame's pooled rows top to bottom. Per pooled row py: 9 waves compute the two new stem rows
-// 2py, 2py+1 (130 pixels, one 16-pixel block per wave, all 64 channels; MFMAs issued
+// One workgroup = one frame x one strip of 40 pooled columns (81 stem columns), walking the
+// frame's pooled rows top to bottom. Per pooled row py: 11 waves compute the two new stem rows
+// 2py, 2py+1 (162 pixels, one 16-pixel block per wave, all 64 channels; MFMAs issued
 // transposed -- weights as the A operand -- so a lane's accumulator holds 4 consecutive channels
 // of one pixel), write them into a 3-row LDS ring (row 2py-1 is still there from the previous
 // row), and pool. Stem outputs are >= 0 (ReLU), so zeros stand for the pool's -inf padding:
@@ -40,15 +40,19 @@ struct StemK {
 
 namespace {
 
-constexpr int SP_PC = 32;                                // pooled columns per workgroup
-constexpr int SP_SC = 2 * SP_PC + 1;                     // stem columns per workgroup (65)
-constexpr int SP_PX = 2 * SP_SC;                         // stem pixels per pooled row (130)
-constexpr int SP_NW = (SP_PX + 15) / 16;                 // waves: one 16-pixel block each (9)
+// 40 pooled columns: 81 stem columns x 2 rows = 162 pixels = 11 waves of 16 (3 / 3 / 3 / 2 per
+// SIMD; 32 columns gave 9 waves, 3 / 2 / 2 / 2, and the 3-wave SIMD set the pace), and a 160-wide
+// pooled map is 4 whole strips
+constexpr int SP_PC = 40;                                // pooled columns per workgroup
+constexpr int SP_SC = 2 * SP_PC + 1;                     // stem columns per workgroup (81)
+constexpr int SP_PX = 2 * SP_SC;                         // stem pixels per pooled row (162)
+constexpr int SP_NW = (SP_PX + 15) / 16;                 // waves: one 16-pixel block each (11)
 constexpr int SP_CO = 64, SP_K = 7;                      // output channels, K-steps (tap rows)
 constexpr int SP_WSTEP = 2 * SP_CO * 64;                 // one K-step of both weight planes (8 KB)
 constexpr int SP_W_BYTES = SP_K * SP_WSTEP;              // 56 KB
-constexpr int SP_ROW = SP_SC * SP_CO * 4;                // one stem row of the strip (16.25 KB)
-constexpr int SP_LDS = SP_W_BYTES + 3 * SP_ROW;          // 105 KB: one workgroup per CU
+constexpr int SP_ROW = SP_SC * SP_CO * 4;                // one stem row of the strip (20.25 KB)
+constexpr int SP_LDS = SP_W_BYTES + 3 * SP_ROW;          // 117 KB: one workgroup per CU
+static_assert(SP_PC * 16 <= SP_NW * 64, "pool phase: one thread per pooled column and 4 channels");
 static_assert(SP_K * 8 > SP_NW, "weight pieces");
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
