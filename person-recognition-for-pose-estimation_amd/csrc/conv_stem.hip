@@ -57,6 +57,13 @@ static_assert(SP_K * 8 > SP_NW, "weight pieces");
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
+// ring layout: stem pixel c's 4-channel group g (16 B) at float offset 4 (g ^ (c & 7)) of its
+// 256-B line. The epilogue's ds_write_b128 is serviced in groups of 8 consecutive lanes = 8
+// consecutive pixels at one g: unswizzled they all hit one bank set (8-way; 42 % of LDS-active
+// cycles were conflicts); swizzled they cover 8 distinct 16-B slots. The pool's reads (16 lanes
+// = all 16 groups of one pixel) stay one contiguous 256-B line.
+__device__ __forceinline__ int rslot(int g, int c) { return (g ^ (c & 7)) * 4; }
+
 __device__ __forceinline__ void lds_barrier() {         // LDS traffic retired + s_barrier, fenced
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -176,7 +183,7 @@ __global__ __launch_bounds__(SP_NW * 64, 1) void stem_pool_kernel(StemK p) {
           v[e] = pvalid && t > 0.f ? t : 0.f;
           ymax = fmaxf(ymax, v[e]);
         }
-        *reinterpret_cast<f4*>(dst + cb * 16 + fg * 4) = v;
+        *reinterpret_cast<f4*>(dst + rslot(cb * 4 + fg, c)) = v;
       }
     }
     lds_barrier();
@@ -185,10 +192,10 @@ __global__ __launch_bounds__(SP_NW * 64, 1) void stem_pool_kernel(StemK p) {
       f4 m = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int dy = -1; dy <= 1; ++dy) {
-        const float* src = ring + (((2 * py + dy + 3) % 3) * SP_SC + 2 * pj) * SP_CO + pc;
+        const float* src = ring + (((2 * py + dy + 3) % 3) * SP_SC + 2 * pj) * SP_CO;
 #pragma unroll
         for (int dx = 0; dx < 3; ++dx) {
-          const f4 v = *reinterpret_cast<const f4*>(src + dx * SP_CO);
+          const f4 v = *reinterpret_cast<const f4*>(src + dx * SP_CO + rslot(pc >> 2, 2 * pj + dx));
 #pragma unroll
           for (int e = 0; e < 4; ++e) m[e] = fmaxf(m[e], v[e]);
         }
