@@ -30,7 +30,8 @@
 // (tests/test_gpu_ops.py: vs fp64 and vs the unfused path).
 //
 // LDS (80 KB, two workgroups per CU): TT [2 chunks][192 px][128 B] (t1, then t2 in its first
-// 32 KB), the swizzled planes layout of conv_halo.hip (slot s of pixel q at s ^ ((q >> 1) & 7));
+// 32 KB), the swizzled planes layout of conv_halo.hip (slot s of pixel q at s ^ swz_halo(column), t2 at
+// s ^ swz_rows(q): conv.h);
 // the W1 / W2 ring [4 stages][2 planes][64 rows][64 B] right after it (three K-steps of
 // lookahead; the block A operand of phase 1 is loaded two K-steps ahead into registers); phase
 // 3's W3 half [2 K-steps][2 planes][128 rows][64 B] overlays TT's last 16 KB and ring stages 0-1.
@@ -99,8 +100,10 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // the fp16 planes (4 x f16 each) of channels c0..c0+3 (c0 % 4 == 0, one 8-channel group) of
 // pixel q into the planes layout: two 8-B LDS writes
-__device__ __forceinline__ void put_planes4(unsigned char* base, int chb, int q, int c0, unsigned long long (&pl)[2]) {
-  const int sw = (q >> 1) & 7, g = (c0 & 31) >> 3;
+// (sw: the pixel's slot swizzle -- swz_halo of its column for t1, swz_rows for t2)
+__device__ __forceinline__ void put_planes4(unsigned char* base, int chb, int q, int sw, int c0,
+                                            unsigned long long (&pl)[2]) {
+  const int g = (c0 & 31) >> 3;
   unsigned char* pq = base + (c0 >> 5) * chb + q * 128 + (c0 & 7) * 2;
   *reinterpret_cast<unsigned long long*>(pq + (((2 * g) ^ sw) << 4)) = pl[0];
   *reinterpret_cast<unsigned long long*>(pq + (((2 * g + 1) ^ sw) << 4)) = pl[1];
@@ -298,7 +301,10 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
     for (int j = 0; j < NJ1; ++j) {
       unsigned long long pl[2];
       split_planes_f16(acc1[i][j], s1, pl);
-      put_planes4(lds, CHB1, (wave + i * NW) * 16 + fr, j * 16 + fg * 4, pl);
+      {
+        const int q1 = (wave + i * NW) * 16 + fr;
+        put_planes4(lds, CHB1, q1, swz_halo(q1 % HW_), j * 16 + fg * 4, pl);
+      }
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // t1 in LDS before the next barrier
@@ -308,7 +314,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
 #pragma unroll
   for (int t = 0; t < 9; ++t) {
     const int px = (wave + t / 3) * HW_ + fr + t % 3;
-    aoff[t] = px * 128 + (((2 * fg) ^ ((px >> 1) & 7)) << 4);
+    aoff[t] = px * 128 + (((2 * fg) ^ swz_halo(px % HW_)) << 4);
   }
   f32x4 acc2[NJ1];
 #pragma unroll
@@ -399,7 +405,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
   for (int j = 0; j < NJ1; ++j) {
     unsigned long long pl[2];
     split_planes_f16(acc2[j], s2, pl);
-    put_planes4(lds, CHB2, wave * 16 + fr, j * 16 + fg * 4, pl);
+    put_planes4(lds, CHB2, wave * 16 + fr, swz_rows(wave * 16 + fr), j * 16 + fg * 4, pl);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // t2 in LDS before the next barrier
   f16x8 xb[NXK][2];
@@ -428,7 +434,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
   const unsigned rvo = ov ? (unsigned)(((int64_t)oy * p.xsh + (int64_t)ox * p.xsw + fg * 4) * 4) : BL_OOB;
   const unsigned yvo = ov ? (unsigned)(((int64_t)oy * p.ysh + (int64_t)ox * p.ysw + fg * 4) * 4) : BL_OOB;
   const int q3 = wave * 16 + fr;
-  const int a3 = q3 * 128 + (((2 * fg) ^ ((q3 >> 1) & 7)) << 4);
+  const int a3 = q3 * 128 + (((2 * fg) ^ swz_rows(q3)) << 4);
   float ymax = 0.f;
   f4 res[PROJ ? 1 : NJ];
 #pragma unroll 1

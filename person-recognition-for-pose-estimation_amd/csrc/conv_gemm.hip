@@ -18,9 +18,9 @@
 // row blocks), fragments of step kt from LDS, MFMAs. Same K order, plane split and
 // per-accumulator MFMA order as conv_wave.hip (bit-identical results, tested).
 //
-// LDS per stage: A [256 rows][8 slots x 16 B] (slot s of row r at s ^ gswz(r)) then B [2 planes]
+// LDS per stage: A [256 rows][8 slots x 16 B] (slot s of row r at s ^ swz_rows(r), conv.h) then B [2 planes]
 // [BN cols][64 B] (conv_wave's swizzle). The epilogue slab reuses stage 0.
-// gswz: a ds_read_b128 is serviced in four 16-lane groups (MI355X_MICROARCH.md, LDS), each
+// swz_rows: a ds_read_b128 is serviced in four 16-lane groups (MI355X_MICROARCH.md, LDS), each
 // holding rows fr = {0-3, 12-15} of one 16-B column slot L and rows {4-11} of slot L ^ 2. With the
 // rows' 128-B pitch, even and odd rows fall in opposite halves of the 256-B bank row, so the slot
 // function must give {f(r)} of one set and {f(r) ^ 2} of the other = all 8 slots per parity:
@@ -33,7 +33,6 @@ namespace {
 
 constexpr int GBK = 32;
 
-__device__ __forceinline__ int gswz(int row) { return (row >> 1) & 5; }
 
 // F16: precision 3 (fp16 planes of the per-frame-scaled activations, the weights' fp16 planes
 // pre-scaled per output channel; the per-row inverse scale in the epilogue), as conv_wave.hip.
@@ -70,7 +69,7 @@ __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
     const int j = wave * PW + i;
     if (j < NA) {
       const int row = j * 8 + (lane >> 3);
-      const int s = (lane & 7) ^ gswz(row);            // logical slot landing in this lane's slot
+      const int s = (lane & 7) ^ swz_rows(row);            // logical slot landing in this lane's slot
       const int m = m0 + row < p.M ? m0 + row : p.M - 1;   // tail rows re-read the last row
       src[i] = p.x + (int64_t)m * p.xsw + s * 4;
       dst[i] = j * 1024;
@@ -142,7 +141,7 @@ __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
         for (int u = PW * i / TM; u < PW * (i + 1) / TM; ++u) piece(u, ks, sn);
       }
       const int row = wm * (BM / WM) + i * 16 + fr;
-      const int sw = gswz(row);
+      const int sw = swz_rows(row);
       const unsigned char* ap = sa + row * 128;
       const f4 v0 = *reinterpret_cast<const f4*>(ap + (((2 * fg) ^ sw) << 4));
       const f4 v1 = *reinterpret_cast<const f4*>(ap + (((2 * fg + 1) ^ sw) << 4));

@@ -16,7 +16,7 @@
 // bit-identical to it (tested).
 //
 // LDS (one array): halo double buffer [2][HQ * 8 px][8 x 16 B] (slot swizzle: logical 16-B
-// slot s of pixel q lives at s ^ ((q >> 1) & 7): 16 consecutive pixels of a fragment read hit
+// slot s of pixel q lives at s ^ swz_halo(column of q) (conv.h): 16 consecutive pixels of a fragment read hit
 // 16 distinct (half-row, slot) pairs -- conflict-free ds_read_b128), B ring [2][2 planes][128
 // cols][64 B] (the wave kernel's swizzle). The epilogue slab reuses the halo buffers.
 //
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     const int px = q * 8 + (lane >> 3);
     const int hr = px / HW_, hc = px - hr * HW_;
     const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-    const int sl = (lane & 7) ^ ((px >> 1) & 7);      // logical slot stored at this lane's slot
+    const int sl = (lane & 7) ^ swz_halo(hc);         // logical slot stored at this lane's slot
     const bool ok = q < HQ && px < HP && (unsigned)ih < (unsigned)p.Hi && (unsigned)iw < (unsigned)p.Wi;
     hvo[k] = ok ? (unsigned)(((int64_t)ih * p.xsh + (int64_t)iw * p.xsw + sl * 4) * 4) : OOB;
   }
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const int px = hb0 + (t / 3) * HW_ + t % 3;
-      const int sw = (px >> 1) & 7;
+      const int sw = swz_halo(px % HW_);
       aoff[i][t] = px * 128 + (((2 * fg) ^ sw) << 4);
     }
   }
