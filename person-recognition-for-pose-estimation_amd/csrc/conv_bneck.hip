@@ -240,6 +240,10 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
   static_assert(RING == 4 && NK1 >= 2, "phase-1 wait counts");
 #pragma unroll
   for (int u = 0; u < RING - 1; ++u) issue_wu(u);
+  // the counted waits below assume this issue order (W pieces, then the A loads); without the
+  // fence the scheduler may hoist the A loads above the LDS-DMA (a build that only added A loads
+  // did so, and W(0) was then not covered by the first wait: wrong results)
+  __builtin_amdgcn_sched_barrier(0);
   load_a(0);
   load_a(1);
   split(0);
@@ -253,6 +257,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
       if (kt == 0 || kt == NK1 - 1) wait_barrier<2 * PPW + 2 * 2>(); else wait_barrier<2 * PPW + 3 * 2>();
     }
     issue_wu(kt + RING - 1);
+    __builtin_amdgcn_sched_barrier(0);                       // W(kt + 3) before A(kt + 2): the counts
     if (kt + 2 < NK1) load_a(kt + 2);
     const unsigned char* sb = lds + RING_OFF + (kt % RING) * STAGE;
 #pragma unroll
@@ -453,6 +458,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
       // every wave is past part h-1's MFMAs: its buffer takes part h + 1 now
       if (h + 1 < NPART) issue_w3(h + 1);
       asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);             // (the counted waits assume this issue order)
     }
     f32x4 acc3[NJ];
 #pragma unroll
@@ -483,6 +489,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
       __builtin_amdgcn_sched_barrier(0);
       issue_w3(h + 1);
       asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);             // (the counted waits assume this issue order)
     }
     // (residual +) bn3 + ReLU: lane (fr, fg) = pixel (oy, ox), channels h*R3 + j*16 + fg*4 .. +3
 #pragma unroll
@@ -500,6 +507,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kern
       bs_f4(yr, v, yvo, (h * R3 + j * 16) * 4);
     }
     asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);             // (the counted waits assume this issue order)
   }
   if (!ov) ymax = 0.f;                                       // (an invalid pixel's y is relu(bias))
   if (p.y_amax) amax_commit(p.y_amax + n, ymax);
