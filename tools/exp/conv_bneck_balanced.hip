@@ -1,0 +1,575 @@
+// Fused ResNet-50 bottleneck with identity shortcut (torchvision Bottleneck.forward, v1.5; the
+// reference's trunk, training/modify_models.py:413-446):
+//   y = relu(bn3(conv3(relu(bn2(conv2_3x3(relu(bn1(conv1(x)))))))) + x)
+// in ONE kernel per 8 x 16 output-pixel tile, precision 3 (two fp16 planes, three MFMA terms).
+//
+// Why: layer1's identity blocks run as three HBM-bound launches (conv1 reads the 256-channel
+// block input, 6.7 GB at bs = 256, writes t1; conv2 reads t1 with its halo and writes t2; conv3
+// reads t2 AND the block input again as the residual and writes y: ~27 GB per block, 7.0 ms,
+// profiles/r03_layer_profile_bufaddr.txt). Here t1 and t2 live only in LDS, the block input is
+// read once (plus the 3x3 halo, mostly L2) and y written once: ~14 GB.
+//
+// Phases of one workgroup (8 waves):
+//   1. t1 = relu(bn1(W1 x)) on the tile's 10 x 18 haloed pixels (12 row blocks of 16), A straight
+//      from global (buffer loads; pixels outside the image read zeros and their t1 is forced to
+//      0 = conv2's zero padding), split into fp16 planes with the frame's scale (x_amax[n], as
+//      the unfused conv1), W1 through an LDS-DMA ring. t1 is then written to LDS as fp16 planes
+//      of t1 * s1 with ONE scale per tile, s1 = 2^(15 - e), max|t1 over the tile| < 2^e (a
+//      block-wide max): t1's operand rounding depends only on this tile of this frame, so frames
+//      stay independent of their batch-mates.
+//   2. t2 = relu(bn2(conv2(t1))): conv_halo.hip's K-loop (9 taps x 2 chunks) on the LDS tile,
+//      planes read without a split; t2 -> LDS as fp16 planes with the tile's scale s2.
+//   3. y = relu(bn3(W3 t2) + x): W3 in two 128-column halves through LDS, residual read from
+//      global, y written from the MFMA accumulator layout, per-frame max|y| raised (y_amax).
+// Every MFMA is issued transposed (weights as the A operand, pixels as B), so a lane's
+// accumulator holds 4 consecutive channels of one pixel: the epilogues write t1 / t2 planes with
+// two 8-B LDS stores per 4 channels and read the residual / store y as 16-B buffer accesses.
+// Epilogue arithmetic as conv_wave.hip (scale16 carries the weights' 2^-e, the activation
+// scale is removed exactly); only t1 / t2 are rounded with per-tile instead of per-frame
+// scales, so results agree with the unfused launches to the precision-3 operand error
+// (tests/test_gpu_ops.py: vs fp64 and vs the unfused path).
+//
+// LDS (80 KB, two workgroups per CU): TT [2 chunks][192 px][128 B] (t1, then t2 in its first
+// 32 KB), the swizzled planes layout of conv_halo.hip (slot s of pixel q at s ^ swz_halo(column), t2 at
+// s ^ swz_rows(q): conv.h);
+// the W1 / W2 ring [4 stages][2 planes][64 rows][64 B] right after it (three K-steps of
+// lookahead; the block A operand of phase 1 is loaded two K-steps ahead into registers); phase
+// 3's W3 half [2 K-steps][2 planes][128 rows][64 B] overlays TT's last 16 KB and ring stages 0-1.
+#include "conv.h"
+
+namespace prpe_k {
+
+struct BneckK {
+  const float* x; int64_t xsn, xsh, xsw; const float* x_amax;
+  float* y; int64_t ysn, ysh, ysw; float* y_amax;
+  int N, H, W;
+  const uint16_t* wh[3]; const uint16_t* wl[3];
+  int kp[3];
+  const float* sc[3]; const float* bi[3];
+  int tiles_w, tiles_h, nwg;
+  int mid;                                               // 64 or 128 (BShape)
+  int proj;                                              // x has mid channels (layer1.0, see BShape)
+};
+
+namespace {
+
+constexpr int BK_ = 32;
+constexpr int TR = 8, TC = 16, NW = 8;
+constexpr int HW_ = TC + 2, HP = (TR + 2) * HW_;        // 18, 180 haloed pixels
+constexpr int NRB1 = (HP + 15) / 16;                     // 12 row blocks of haloed pixels
+constexpr int CHB1 = NRB1 * 16 * 128;                    // bytes of one 32-channel chunk of t1
+constexpr int CHB2 = TR * TC * 128;                      // ... of t2
+constexpr int W3_PART = 32 * 1024;                       // one W3 part (below) in the overlay
+constexpr int RING = 4;                                  // W1 / W2 ring stages (3 K-steps of lookahead)
+
+// Block shape. MID = the inner width (64: layer1, 128: layer2), CIO = 4 MID output channels.
+// Identity (layer1.1-2, layer2.1-3): x has CIO channels and is the residual; conv3 (K = MID)
+// runs in parts of R3 output columns. Projection (PROJ, layer1.0): x has MID channels, conv3 and
+// the downsample projection are one dual GEMM over [t2 | x] (the engine's pk_dual pack, K = 2 MID,
+// W' = [s3 W3 | sd Wd]), run in four parts of 64 columns; no residual read.
+// LDS: TT (t1, then t2 in its first (MID/32) CHB2 bytes), then the W1 / W2 ring; a W3 part
+// overlays TT past t2 (and, at MID 64, ring stages 0-1). MID 64: 48 + 32 = 80 KB, two
+// workgroups per CU; MID 128: 96 + 64 = 160 KB, one.
+template <int MIDT, bool PROJ> struct BShape {
+  static constexpr int MID = MIDT, CIO = 4 * MIDT;
+  static constexpr int CIN = PROJ ? MID : CIO;           // x channels
+  static constexpr int NK1 = CIN / BK_;                  // phase-1 K-steps
+  static constexpr int NKS3 = PROJ ? 2 * MID / BK_ : MID / BK_;   // phase-3 K-steps
+  static constexpr int R3 = PROJ || MID > 64 ? 64 : 128; // output columns per phase-3 part
+  static constexpr int NPART = CIO / R3;
+  static constexpr int W3_STEP = 2 * R3 * 64;            // one K-step of a part (both planes)
+  static constexpr int TT_BYTES = (MID / 32) * CHB1;
+  static constexpr int STAGE = 2 * MID * 64;             // one K-step of W1 / W2 (both planes)
+  static constexpr int PPW = STAGE / 1024 / NW;          // its LDS-DMA pieces per wave
+  static constexpr int RING_OFF = TT_BYTES;
+  static constexpr int W3_OFF = (MID / 32) * CHB2;       // after t2
+  static constexpr int LDS_BYTES = TT_BYTES + RING * STAGE;
+  static constexpr int WPC = LDS_BYTES <= 80 * 1024 ? 2 : 1;   // workgroups per CU
+  // two W3 part buffers when the free LDS of phase 3 holds them (MID 128: TT past t2 + ring
+  // stages 0-1): part h + 1 is then DMA'd under part h's MFMAs instead of after them
+  static constexpr bool W3DB = W3_OFF + 2 * W3_PART <= RING_OFF + 2 * STAGE;
+  static_assert(!PROJ || MID == 64, "projection block: layer1.0 only");
+  static_assert(PPW >= 1 && STAGE == PPW * NW * 1024, "W ring pieces");
+  static_assert(NKS3 * W3_STEP == W3_PART, "W3 part size");
+  static_assert(NKS3 * 2 * (R3 / 16) == 4 * NW, "4 W3 pieces per wave and part");
+  static_assert(W3_OFF + W3_PART <= RING_OFF + 2 * STAGE, "W3 part overlay below ring stage 2");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS");
+};
+
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+
+// the fp16 planes (4 x f16 each) of channels c0..c0+3 (c0 % 4 == 0, one 8-channel group) of
+// pixel q into the planes layout: two 8-B LDS writes
+// (sw: the pixel's slot swizzle -- swz_halo of its column for t1, swz_rows for t2)
+__device__ __forceinline__ void put_planes4(unsigned char* base, int chb, int q, int sw, int c0,
+                                            unsigned long long (&pl)[2]) {
+  const int g = (c0 & 31) >> 3;
+  unsigned char* pq = base + (c0 >> 5) * chb + q * 128 + (c0 & 7) * 2;
+  *reinterpret_cast<unsigned long long*>(pq + (((2 * g) ^ sw) << 4)) = pl[0];
+  *reinterpret_cast<unsigned long long*>(pq + (((2 * g + 1) ^ sw) << 4)) = pl[1];
+}
+
+// 16 B per lane out through a buffer descriptor (offsets past num_records are dropped)
+__device__ __forceinline__ void bs_f4(__amdgpu_buffer_rsrc_t r, f4 v, unsigned voff, int soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, voff, soff, 0);
+}
+
+// B fragments of column block j from a [2 planes][rows][64 B] stage (conv_wave's slot swizzle)
+__device__ __forceinline__ void b_frags(const unsigned char* sb, int rows, int j, int fr, int fg, f16x8 (&b)[2]) {
+  const int nrow = j * 16 + fr;
+  const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
+  b[0] = *reinterpret_cast<const f16x8*>(bp);
+  b[1] = *reinterpret_cast<const f16x8*>(bp + rows * 64);
+}
+
+// the three partial products of the split, smallest first (conv_wave.hip's order), computed
+// transposed: the weight fragment is the MFMA's A operand and the activation fragment its B, so
+// a lane's accumulator holds 4 consecutive CHANNELS of one pixel (16-B epilogue accesses)
+__device__ __forceinline__ f32x4 mfma3t(const f16x8 (&w)[2], const f16x8 (&a)[2], f32x4 c) {
+  c = mfma16(w[0], a[1], c);
+  c = mfma16(w[1], a[0], c);
+  c = mfma16(w[0], a[0], c);
+  return c;
+}
+
+template <int MIDT, bool PROJ>
+__global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kernel(BneckK p) {
+  using S = BShape<MIDT, PROJ>;
+  constexpr int MID = S::MID, CIO = S::CIO, CIN = S::CIN, NK1 = S::NK1, R3 = S::R3, W3_STEP = S::W3_STEP;
+  constexpr int STAGE = S::STAGE, PPW = S::PPW, RING_OFF = S::RING_OFF, W3_OFF = S::W3_OFF;
+  constexpr int NJ1 = MID / 16;                              // 16-channel column blocks of t1 / t2
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[S::LDS_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fg = lane >> 4;
+  int L = xcd_remap(blockIdx.x, p.nwg);
+  const int tw = L % p.tiles_w;
+  L /= p.tiles_w;
+  const int th = L % p.tiles_h;
+  const int n = L / p.tiles_h;
+  const int oh0 = th * TR, ow0 = tw * TC;
+
+  // ---- descriptors: this frame of x (phase 1 A and the residual), the six weight planes
+  const float* xn = p.x + (int64_t)n * p.xsn;
+  const int frame_bytes = (int)(((int64_t)(p.H - 1) * p.xsh + (int64_t)(p.W - 1) * p.xsw + CIN) * 4);
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(xn, frame_bytes);
+  __amdgpu_buffer_rsrc_t wr[3][2];
+#pragma unroll
+  for (int l = 0; l < 3; ++l) {
+    const int rows = l == 2 ? CIO : MID;
+    wr[l][0] = buf_rsrc(p.wh[l], rows * p.kp[l] * 2);
+    wr[l][1] = buf_rsrc(p.wl[l], rows * p.kp[l] * 2);
+  }
+  // W1 / W2 ring pieces of this wave: piece j = wave PPW + i -> plane j / NJ1 (= the wave's
+  // plane: waves 0-3 the hi plane, 4-7 the lo), rows 16 (j % NJ1) .. +16. The plane's descriptors
+  // are selected once (wave-uniform SGPRs: a per-piece select spilled them to scratch)
+  static_assert(NJ1 % PPW == 0 && PPW * NW == 2 * NJ1, "W ring piece map");
+  const bool bq = wave * PPW / NJ1 != 0;
+  const __amdgpu_buffer_rsrc_t wq0 = bq ? wr[0][1] : wr[0][0], wq1 = bq ? wr[1][1] : wr[1][0];
+  int bnrow[PPW], bch[PPW], bdst[PPW];
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int j = wave * PPW + i;
+    bnrow[i] = (j % NJ1) * 16 + (lane >> 2);
+    bch[i] = (lane & 3) ^ swzF(bnrow[i]);
+    bdst[i] = RING_OFF + ((j / NJ1) * MID + (j % NJ1) * 16) * 64;
+  }
+  auto issue_w = [&](int l, int kt, int stage) {           // l = 0 (W1) or 1 (W2)
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const unsigned vo = (unsigned)((bnrow[i] * p.kp[l] + bch[i] * 8) * 2);
+      bl_lds16(l ? wq1 : wq0, lds + bdst[i] + stage * STAGE, vo, kt * BK_ * 2);
+    }
+  };
+  // the W stream: steps u < NK1 are W1's K-steps, the next 18 W2's; step u goes to stage u % RING
+  constexpr int NK2 = (MID / 32) * 9, NU = NK1 + NK2;
+  auto issue_wu = [&](int u) {
+    if (u < NK1) issue_w(0, u, u % RING);
+    else if (u < NU) issue_w(1, u - NK1, u % RING);
+  };
+
+  // =========================== phase 1: t1 on the haloed tile
+  const float am = p.x_amax[n];
+  const int ex = f16_scale_exp(am);
+  const float sa = ldexpf(1.f, 15 - ex), inv0 = ldexpf(1.f, ex - 15);
+  // 12 haloed row blocks x NJ1 column blocks over 8 waves, balanced: wave w takes row block w
+  // (all column blocks) and half the column blocks of row block rb1 = 8 + w / 2 (half jh = w & 1),
+  // so every wave issues 1.5 row blocks' MFMAs (two for waves 0-3 and one for 4-7 set the pace
+  // before; both waves of a pair load rb1's activations, the second from L2)
+  static_assert(NRB1 == NW + NW / 2 && NJ1 % 2 == 0, "phase-1 wave map");
+  constexpr int NH = NJ1 / 2;
+  const int jh = wave & 1;
+  const int rb1 = NW + (wave >> 1);
+  unsigned av[2];
+  bool pv[2];                                                // that pixel is inside the image
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int rb = i == 0 ? wave : rb1;
+    const int px = rb * 16 + fr;
+    const int hr = px / HW_, hc = px - hr * HW_;
+    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
+    pv[i] = px < HP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && rb < NRB1;
+    av[i] = pv[i] ? (unsigned)(((int64_t)ih * p.xsh + (int64_t)iw * p.xsw + fg * 8) * 4) : BL_OOB;
+  }
+  f32x4 acc1[NJ1], acc1b[NH];                                // row block w; half of row block rb1
+#pragma unroll
+  for (int j = 0; j < NJ1; ++j) acc1[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < NH; ++j) acc1b[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // A straight from global into registers, two K-steps ahead (raw[step & 1])
+  f4 raw[2][2][2];
+  auto load_a = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      raw[kt & 1][i][0] = bl_f4(xr, av[i], kt * BK_ * 4);
+      raw[kt & 1][i][1] = bl_f4(xr, av[i] + 16, kt * BK_ * 4);
+    }
+  };
+  f16x8 af[2][2];
+  auto split = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      unsigned long long p0[2], p1[2];
+      split_planes_f16(raw[kt & 1][i][0], sa, p0);
+      split_planes_f16(raw[kt & 1][i][1], sa, p1);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        af[i][q] = __builtin_bit_cast(f16x8, u64x2{p0[q], p1[q]});
+      }
+    }
+  };
+  // Per step kt: [wait + barrier] W(kt + RING - 1), A(kt + 2) issued, MFMAs on A(kt), split of
+  // A(kt + 1). The wait leaves in flight exactly the ops issued after this wave's pieces of
+  // W(kt) (counted per step below: PPW pieces per W step, na = A loads per step), so A stays two
+  // steps ahead.
+  static_assert(RING == 4 && NK1 >= 2, "phase-1 wait counts");
+#pragma unroll
+  for (int u = 0; u < RING - 1; ++u) issue_wu(u);
+  // the counted waits below assume this issue order (W pieces, then the A loads); without the
+  // fence the scheduler may hoist the A loads above the LDS-DMA (a build that only added A loads
+  // did so, and W(0) was then not covered by the first wait: wrong results)
+  __builtin_amdgcn_sched_barrier(0);
+  load_a(0);
+  load_a(1);
+  split(0);
+#pragma unroll
+  for (int kt = 0; kt < NK1; ++kt) {
+    // ops issued after W(kt): kt = 0: W1, W2, A0, A1; middle steps: 2 W + 3 A steps (fewer only
+    // where the count is not needed: W(1), W(2) precede A(0)); last: 2 W + 2 A steps
+    // (4 A loads per step: two row blocks, two 16-B loads each)
+    if (kt == 0 || kt == NK1 - 1) wait_barrier<2 * PPW + 2 * 4>(); else wait_barrier<2 * PPW + 3 * 4>();
+    issue_wu(kt + RING - 1);
+    __builtin_amdgcn_sched_barrier(0);                       // W(kt + 3) before A(kt + 2): the counts
+    if (kt + 2 < NK1) load_a(kt + 2);
+    const unsigned char* sb = lds + RING_OFF + (kt % RING) * STAGE;
+#pragma unroll
+    for (int j = 0; j < NJ1; ++j) {
+      f16x8 b[2];
+      b_frags(sb, MID, j, fr, fg, b);
+      acc1[j] = mfma3t(b, af[0], acc1[j]);
+    }
+#pragma unroll
+    for (int jj = 0; jj < NH; ++jj) {                        // this wave's half of row block rb1
+      f16x8 b[2];
+      b_frags(sb, MID, jh * NH + jj, fr, fg, b);
+      acc1b[jj] = mfma3t(b, af[1], acc1b[jj]);
+    }
+    if (kt + 1 < NK1) split(kt + 1);
+  }
+  // epilogue 1: bn1 + ReLU (zero outside the image: conv2's padding), tile max, planes -> TT.
+  // Lane (fr, fg) holds channels j*16 + fg*4 .. +3 of pixel rb*16 + fr.
+  float m1 = 0.f;
+  auto epi1 = [&](f32x4& a, int cb, bool valid) {
+    const int c0 = cb * 16 + fg * 4;
+    const f4 s = *reinterpret_cast<const f4*>(p.sc[0] + c0), b = *reinterpret_cast<const f4*>(p.bi[0] + c0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = fmaf(a[r] * inv0, s[r], b[r]);
+      v = v > 0.f && valid ? v : 0.f;
+      a[r] = v;
+      m1 = fmaxf(m1, v);
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < NJ1; ++j) epi1(acc1[j], j, pv[0]);
+#pragma unroll
+  for (int jj = 0; jj < NH; ++jj) epi1(acc1b[jj], jh * NH + jj, pv[1]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m1 = fmaxf(m1, __shfl_xor(m1, o, 64));
+  wait_barrier<0>();                                         // every wave's phase-1 reads of the ring done
+  // tile max through per-wave slots in the ring stage of W1's last step (dead now; the next DMA
+  // into it, W(NK1 + 3), is issued only after phase 2's first barrier): no zeroing, no atomics
+  float* const wmax1 = reinterpret_cast<float*>(lds + RING_OFF + ((NK1 - 1) % RING) * STAGE);
+  if (lane == 0) wmax1[wave] = m1;
+  __syncthreads();
+  m1 = wmax1[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) m1 = fmaxf(m1, wmax1[w]);
+  const int e1 = f16_scale_exp(m1);
+  const float s1 = ldexpf(1.f, 15 - e1), inv1 = ldexpf(1.f, e1 - 15);
+#pragma unroll
+  for (int j = 0; j < NJ1; ++j) {
+    unsigned long long pl[2];
+    split_planes_f16(acc1[j], s1, pl);
+    const int q1 = wave * 16 + fr;
+    put_planes4(lds, CHB1, q1, swz_halo(q1 % HW_), j * 16 + fg * 4, pl);
+  }
+#pragma unroll
+  for (int jj = 0; jj < NH; ++jj) {
+    unsigned long long pl[2];
+    split_planes_f16(acc1b[jj], s1, pl);
+    const int q1 = rb1 * 16 + fr;
+    put_planes4(lds, CHB1, q1, swz_halo(q1 % HW_), (jh * NH + jj) * 16 + fg * 4, pl);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // t1 in LDS before the next barrier
+
+  // =========================== phase 2: t2 = conv2(t1), the halo K-loop on the LDS tile
+  int aoff[9];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    const int px = (wave + t / 3) * HW_ + fr + t % 3;
+    aoff[t] = px * 128 + (((2 * fg) ^ swz_halo(px % HW_)) << 4);
+  }
+  f32x4 acc2[NJ1];
+#pragma unroll
+  for (int j = 0; j < NJ1; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  static_assert(RING == 4, "phase-2 wait counts");
+  int u = NK1;
+#pragma unroll 1
+  for (int c = 0; c < MID / 32; ++c) {
+    const unsigned char* tc = lds + c * CHB1;
+#pragma unroll
+    for (int t = 0; t < 9; ++t, ++u) {
+      // W stream step u (its first RING - 1 were issued during phase 1): in flight after this
+      // wave's pieces of W(u) are those of W(u+1), W(u+2) -- fewer in the last two steps
+      if (c == MID / 32 - 1 && t >= 7) wait_barrier<0>(); else wait_barrier<(RING - 2) * PPW>();
+      issue_wu(u + RING - 1);
+      f16x8 a[2];
+      a[0] = *reinterpret_cast<const f16x8*>(tc + aoff[t]);
+      a[1] = *reinterpret_cast<const f16x8*>(tc + (aoff[t] ^ 16));
+      const unsigned char* sb = lds + RING_OFF + (u % RING) * STAGE;
+#pragma unroll
+      for (int j = 0; j < NJ1; ++j) {
+        f16x8 b[2];
+        b_frags(sb, MID, j, fr, fg, b);
+        acc2[j] = mfma3t(b, a, acc2[j]);
+      }
+    }
+  }
+  // epilogue 2: bn2 + ReLU, tile max, planes -> TT (t1 is dead once every wave is past here).
+  // Lane (fr, fg): output pixel (oh0 + wave, ow0 + fr), channels j*16 + fg*4 .. +3.
+  const int oy = oh0 + wave, ox = ow0 + fr;
+  const bool ov = oy < p.H && ox < p.W;
+  float m2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < NJ1; ++j) {
+    const int c0 = j * 16 + fg * 4;
+    const f4 s = *reinterpret_cast<const f4*>(p.sc[1] + c0), b = *reinterpret_cast<const f4*>(p.bi[1] + c0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float v = fmaf(acc2[j][r] * inv1, s[r], b[r]);
+      v = v > 0.f && ov ? v : 0.f;
+      acc2[j][r] = v;
+      m2 = fmaxf(m2, v);
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m2 = fmaxf(m2, __shfl_xor(m2, o, 64));
+  wait_barrier<0>();                                         // all t1 / W2 reads done, TT and ring free
+  float* const wmax2 = reinterpret_cast<float*>(lds + RING_OFF + 2 * STAGE);   // past the W3 overlay
+  if (lane == 0) wmax2[wave] = m2;
+  // PROJ: the downsample operand, x at this lane's output pixel (channels ks*32 + fg*8 .. +7),
+  // loaded now (older than every W3 piece, so the counted waits below stay exact)
+  constexpr int NXK = PROJ ? MID / BK_ : 1;
+  f4 xc[NXK][2];
+  if constexpr (PROJ) {
+    const unsigned cvo = ov ? (unsigned)(((int64_t)oy * p.xsh + (int64_t)ox * p.xsw + fg * 8) * 4) : BL_OOB;
+#pragma unroll
+    for (int ks = 0; ks < NXK; ++ks) {
+      xc[ks][0] = bl_f4(xr, cvo, ks * BK_ * 4);
+      xc[ks][1] = bl_f4(xr, cvo + 16, ks * BK_ * 4);
+    }
+  }
+  // W3 part h (R3 output columns, all NKS3 K-steps, both planes) into the overlay (TT past t2 +
+  // ring stages 0-1; buffer h & 1 when double-buffered): 32 pieces, 4 per wave
+  constexpr bool W3DB = S::W3DB;
+  auto issue_w3 = [&](int h) {
+    unsigned char* const w3b = lds + W3_OFF + (W3DB ? (h & 1) * W3_PART : 0);
+    constexpr int RB3 = R3 / 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int idx = wave * 4 + i;
+      const int rb = idx % RB3, q = (idx / RB3) & 1, ks = idx / (2 * RB3);
+      const int nrow = rb * 16 + (lane >> 2);
+      const int ch = (lane & 3) ^ swzF(nrow);
+      const unsigned vo = (unsigned)(((h * R3 + nrow) * p.kp[2] + ch * 8) * 2);
+      bl_lds16(q ? wr[2][1] : wr[2][0], w3b + ks * W3_STEP + (q * R3 + rb * 16) * 64, vo, ks * BK_ * 2);
+    }
+  };
+  issue_w3(0);
+  __syncthreads();
+  m2 = wmax2[0];
+#pragma unroll
+  for (int w = 1; w < NW; ++w) m2 = fmaxf(m2, wmax2[w]);
+  // PROJ: t2 and x feed one accumulator, so they share one scale (their maxima combined, as
+  // prpe_conv2d's dual-input GEMM); the x bound is per frame, t2's per tile
+  const int e2 = f16_scale_exp(PROJ ? fmaxf(m2, am) : m2);
+  const float s2 = ldexpf(1.f, 15 - e2), inv2 = ldexpf(1.f, e2 - 15);
+#pragma unroll
+  for (int j = 0; j < NJ1; ++j) {
+    unsigned long long pl[2];
+    split_planes_f16(acc2[j], s2, pl);
+    put_planes4(lds, CHB2, wave * 16 + fr, swz_rows(wave * 16 + fr), j * 16 + fg * 4, pl);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");        // t2 in LDS before the next barrier
+  f16x8 xb[NXK][2];
+  if constexpr (PROJ) {
+#pragma unroll
+    for (int ks = 0; ks < NXK; ++ks) {
+      unsigned long long p0[2], p1[2];
+      split_planes_f16(xc[ks][0], s2, p0);
+      split_planes_f16(xc[ks][1], s2, p1);
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        xb[ks][q] = __builtin_bit_cast(f16x8, u64x2{p0[q], p1[q]});
+      }
+    }
+  }
+
+  // =========================== phase 3: y = relu(bn3(W3 t2) + x) in NPART parts of R3 columns
+  // (PROJ: y = relu(W' [t2 | x] + b3 + bd)). Residual loads and y stores are 16-B buffer
+  // accesses (an invalid pixel's offset is past the descriptor: zeros / dropped), issued
+  // unconditionally so every wave counts the same vmcnt.
+  constexpr int NPART = S::NPART, NKS3 = S::NKS3, NJ = R3 / 16;
+  constexpr int NRES = PROJ ? 0 : NJ;                        // residual loads per part
+  const int yframe_bytes = (int)(((int64_t)(p.H - 1) * p.ysh + (int64_t)(p.W - 1) * p.ysw + CIO) * 4);
+  const __amdgpu_buffer_rsrc_t yr = buf_rsrc(p.y + (int64_t)n * p.ysn, yframe_bytes);
+  const unsigned rvo = ov ? (unsigned)(((int64_t)oy * p.xsh + (int64_t)ox * p.xsw + fg * 4) * 4) : BL_OOB;
+  const unsigned yvo = ov ? (unsigned)(((int64_t)oy * p.ysh + (int64_t)ox * p.ysw + fg * 4) * 4) : BL_OOB;
+  const int q3 = wave * 16 + fr;
+  const int a3 = q3 * 128 + (((2 * fg) ^ swz_rows(q3)) << 4);
+  float ymax = 0.f;
+  f4 res[PROJ ? 1 : NJ];
+#pragma unroll 1
+  for (int h = 0; h < NPART; ++h) {
+    if constexpr (!PROJ) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) res[j] = bl_f4(xr, rvo, (h * R3 + j * 16) * 4);
+    }
+    if (h == 0) {
+      wait_barrier<NRES>();                                  // t2 written (W3 part 0 landed at the __syncthreads)
+    } else {
+      // W3 part h was issued before part h-1's NJ stores and this part's residual loads
+      wait_barrier<NJ + NRES>();
+    }
+    if constexpr (W3DB) {
+      // every wave is past part h-1's MFMAs: its buffer takes part h + 1 now
+      if (h + 1 < NPART) issue_w3(h + 1);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);             // (the counted waits assume this issue order)
+    }
+    f32x4 acc3[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc3[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKS3; ++ks) {
+      f16x8 a[2];
+      if (ks < MID / BK_) {
+        a[0] = *reinterpret_cast<const f16x8*>(lds + ks * CHB2 + a3);
+        a[1] = *reinterpret_cast<const f16x8*>(lds + ks * CHB2 + (a3 ^ 16));
+      } else {
+        a[0] = xb[ks - MID / BK_ < NXK ? ks - MID / BK_ : 0][0];
+        a[1] = xb[ks - MID / BK_ < NXK ? ks - MID / BK_ : 0][1];
+      }
+      const unsigned char* sb = lds + W3_OFF + (W3DB ? (h & 1) * W3_PART : 0) + ks * W3_STEP;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        f16x8 b[2];
+        b_frags(sb, R3, j, fr, fg, b);
+        acc3[j] = mfma3t(b, a, acc3[j]);
+      }
+    }
+    if (!W3DB && h + 1 < NPART) {
+      // every wave is done reading W3 part h (its ds_reads fed the MFMAs above): overwrite it
+      // with part h + 1 now, BEFORE this part's stores
+      __builtin_amdgcn_sched_barrier(0);
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      issue_w3(h + 1);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);             // (the counted waits assume this issue order)
+    }
+    // (residual +) bn3 + ReLU: lane (fr, fg) = pixel (oy, ox), channels h*R3 + j*16 + fg*4 .. +3
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c0 = h * R3 + j * 16 + fg * 4;
+      const f4 s = *reinterpret_cast<const f4*>(p.sc[2] + c0), b = *reinterpret_cast<const f4*>(p.bi[2] + c0);
+      f4 v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = fmaf(acc3[j][r] * inv2, s[r], b[r]);
+        if constexpr (!PROJ) t += res[j][r];
+        v[r] = t > 0.f ? t : 0.f;
+        ymax = fmaxf(ymax, v[r]);
+      }
+      bs_f4(yr, v, yvo, (h * R3 + j * 16) * 4);
+    }
+    asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);             // (the counted waits assume this issue order)
+  }
+  if (!ov) ymax = 0.f;                                       // (an invalid pixel's y is relu(bias))
+  if (p.y_amax) amax_commit(p.y_amax + n, ymax);
+}
+
+}  // namespace
+
+int bneck_launch(const BneckK& kp0, hipStream_t st) {
+  BneckK kp = kp0;
+  kp.tiles_w = (kp.W + TC - 1) / TC;
+  kp.tiles_h = (kp.H + TR - 1) / TR;
+  const int64_t nwg = (int64_t)kp.N * kp.tiles_w * kp.tiles_h;
+  if (nwg <= 0 || nwg >= (1LL << 31)) return PRPE_EINVAL;
+  kp.nwg = (int)nwg;
+  if (kp.proj) hipLaunchKernelGGL((bneck_kernel<64, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  else if (kp.mid == 64) hipLaunchKernelGGL((bneck_kernel<64, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  else hipLaunchKernelGGL((bneck_kernel<128, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  return launch_status();
+}
+
+}  // namespace prpe_k
+
+extern "C" int prpe_bottleneck(const prpe_bneck_desc* d, void* stream) {
+  using namespace prpe_k;
+  if (!d || !view_ok(&d->x) || !view_ok(&d->y) || !d->x_amax) return PRPE_EINVAL;
+  const prpe_view& x = d->x; const prpe_view& y = d->y;
+  const int MID = d->mid, CIO = 4 * d->mid;
+  const bool proj = x.c == MID;                          // projection block (layer1.0)
+  if ((MID != 64 && MID != 128) || (proj && MID != 64) || (x.c != CIO && !proj) || y.c != CIO || x.n != y.n ||
+      x.h != y.h || x.w != y.w)
+    return PRPE_EINVAL;
+  if (x.sc != 1 || y.sc != 1 || x.sw % 4 || x.sh % 4 || x.sn % 4 || (uintptr_t)x.ptr % 16 || x.sw < 0 || x.sh < 0 ||
+      y.sw % 4 || y.sh % 4 || y.sn % 4 || (uintptr_t)y.ptr % 16 || y.sw < 0 || y.sh < 0)
+    return PRPE_EINVAL;
+  const int kneed[3] = {(int)x.c, 9 * MID, proj ? 2 * MID : MID};
+  for (int l = 0; l < 3; ++l) {
+    if (!d->w_h16[l] || !d->w_l16[l] || !d->scale16[l] || !d->bias[l] || d->k_pad[l] != kneed[l]) return PRPE_EINVAL;
+    if ((uintptr_t)d->w_h16[l] % 16 || (uintptr_t)d->w_l16[l] % 16 || (uintptr_t)d->scale16[l] % 16 ||
+        (uintptr_t)d->bias[l] % 16)
+      return PRPE_EINVAL;
+  }
+  if (((int64_t)(x.h - 1) * x.sh + (int64_t)(x.w - 1) * x.sw + x.c) * 4 >= (1LL << 31) ||
+      ((int64_t)(y.h - 1) * y.sh + (int64_t)(y.w - 1) * y.sw + CIO) * 4 >= (1LL << 31))
+    return PRPE_EINVAL;
+  BneckK kp{};
+  kp.x = x.ptr; kp.xsn = x.sn; kp.xsh = x.sh; kp.xsw = x.sw; kp.x_amax = d->x_amax;
+  kp.y = y.ptr; kp.ysn = y.sn; kp.ysh = y.sh; kp.ysw = y.sw; kp.y_amax = d->y_amax;
+  kp.N = x.n; kp.H = x.h; kp.W = x.w;
+  kp.proj = proj ? 1 : 0;
+  kp.mid = MID;
+  for (int l = 0; l < 3; ++l) {
+    kp.wh[l] = d->w_h16[l]; kp.wl[l] = d->w_l16[l]; kp.kp[l] = d->k_pad[l];
+    kp.sc[l] = d->scale16[l]; kp.bi[l] = d->bias[l];
+  }
+  return bneck_launch(kp, as_stream(stream));
+}
