@@ -133,7 +133,7 @@ __device__ __forceinline__ f32x4 mfma3t(const f16x8 (&w)[2], const f16x8 (&a)[2]
 }
 
 template <int MIDT, bool PROJ>
-__global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kernel(BneckK p) {
+__global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void bneck_kernel(BneckK p) {
   using S = BShape<MIDT, PROJ>;
   constexpr int MID = S::MID, CIO = S::CIO, CIN = S::CIN, NK1 = S::NK1, R3 = S::R3, W3_STEP = S::W3_STEP;
   constexpr int STAGE = S::STAGE, PPW = S::PPW, RING_OFF = S::RING_OFF, W3_OFF = S::W3_OFF;
