@@ -5,6 +5,7 @@ set -o pipefail
 O=gpurun_out
 mkdir -p $O
 for a in "" "--proj" "--mid 128"; do timeout -k 10 200 python tools/bneck_bench.py --batch 256 --iters 10 --fused-only $a >> $O/r03ab_bneck_bench_shipped.txt 2>&1 || exit 8; done
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/r03ab_bench_shipped.json 2> $O/r03ab_bench_shipped.err || exit 8
 cp tools/exp/conv_bneck_balanced.hip person-recognition-for-pose-estimation_amd/csrc/conv_bneck.hip
 timeout -k 10 600 python person-recognition-for-pose-estimation_amd/build.py --jobs 16 > $O/r03ab_build.log 2>&1 || exit 9
 timeout -k 10 300 python -u -m pytest tests/test_gpu_bneck.py -x -q --timeout 120 --timeout-method thread > $O/r03ab_bneck_tests.log 2>&1 || exit 1
