@@ -132,8 +132,10 @@ __device__ __forceinline__ f32x4 mfma3t(const f16x8 (&w)[2], const f16x8 (&a)[2]
   return c;
 }
 
+// launch bound: HIP's second argument is waves per SIMD, so WPC workgroups of NW waves per CU =
+// WPC * NW / 4 (caps VGPRs at 128 for the 80-KB shapes; measured neutral, tools/run_r03ac.sh)
 template <int MIDT, bool PROJ>
-__global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC)) void bneck_kernel(BneckK p) {
+__global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void bneck_kernel(BneckK p) {
   using S = BShape<MIDT, PROJ>;
   constexpr int MID = S::MID, CIO = S::CIO, CIN = S::CIN, NK1 = S::NK1, R3 = S::R3, W3_STEP = S::W3_STEP;
   constexpr int STAGE = S::STAGE, PPW = S::PPW, RING_OFF = S::RING_OFF, W3_OFF = S::W3_OFF;
