@@ -168,7 +168,8 @@ int prpe_conv2d(const prpe_conv_desc* d, void* stream);
  * bias[2] = b3 + bd; t2 and x share one power-of-2 scale (max of the tile's max|t2| and the
  * frame's max|x|), as prpe_conv2d's dual-input GEMM.
  * x, y, the weight planes, scale16 and bias 16-B aligned, x / y pixel strides multiples of 4
- * floats, one frame of x and of y < 2^31 bytes; anything else returns -EINVAL.
+ * floats, one frame of x and of y < 2^31 bytes; anything else returns -EINVAL. Not in place: y
+ * must not overlap x (other tiles read x's halo and residual while y is written) -> -EINVAL.
  */
 typedef struct prpe_bneck_desc {
   prpe_view x;
@@ -196,7 +197,7 @@ int prpe_bottleneck(const prpe_bneck_desc* d, void* stream);
  * stem value equals prpe_conv2d's on the same view bit for bit; the stem map never reaches HBM.
  * y: [N, H/4, W/4, 64], channel-contiguous, 16-B aligned; y_amax (optional) raised to max|y[n]|
  * (= the stem map's max: every stem output lies in some window). H, W multiples of 4, one frame
- * of x < 2^31 bytes; anything else returns -EINVAL.
+ * of x < 2^31 bytes, y not overlapping x's N frames; anything else returns -EINVAL.
  */
 typedef struct prpe_stem_desc {
   const float* x;

@@ -280,3 +280,24 @@ __device__ __forceinline__ int swzF(int row) { return (0x78 >> (((row >> 2) & 3)
 static inline bool view_ok(const prpe_view* v) {
   return v && v->ptr && v->n > 0 && v->h > 0 && v->w > 0 && v->c > 0;
 }
+
+// byte range [lo, hi) a view can touch (float elements; negative strides included)
+static inline void view_span(const prpe_view& v, uintptr_t& lo, uintptr_t& hi) {
+  const int64_t ext[4] = {(int64_t)(v.n - 1) * v.sn, (int64_t)(v.h - 1) * v.sh, (int64_t)(v.w - 1) * v.sw,
+                          (int64_t)(v.c - 1) * v.sc};
+  int64_t a = 0, b = 0;
+  for (int i = 0; i < 4; ++i) (ext[i] < 0 ? a : b) += ext[i];
+  lo = (uintptr_t)v.ptr + a * 4;
+  hi = (uintptr_t)v.ptr + (b + 1) * 4;
+}
+// do two byte ranges intersect (kernels that read one tensor's neighbourhood while writing the
+// other must not run in place)
+static inline bool spans_overlap(uintptr_t alo, uintptr_t ahi, uintptr_t blo, uintptr_t bhi) {
+  return alo < bhi && blo < ahi;
+}
+static inline bool views_overlap(const prpe_view& a, const prpe_view& b) {
+  uintptr_t alo, ahi, blo, bhi;
+  view_span(a, alo, ahi);
+  view_span(b, blo, bhi);
+  return spans_overlap(alo, ahi, blo, bhi);
+}

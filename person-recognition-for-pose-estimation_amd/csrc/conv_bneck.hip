@@ -536,6 +536,7 @@ extern "C" int prpe_bottleneck(const prpe_bneck_desc* d, void* stream) {
   using namespace prpe_k;
   if (!d || !view_ok(&d->x) || !view_ok(&d->y) || !d->x_amax) return PRPE_EINVAL;
   const prpe_view& x = d->x; const prpe_view& y = d->y;
+  if (views_overlap(x, y)) return PRPE_EINVAL;            // not in place (prpe.h)
   const int MID = d->mid, CIO = 4 * d->mid;
   const bool proj = x.c == MID;                          // projection block (layer1.0)
   if ((MID != 64 && MID != 128) || (proj && MID != 64) || (x.c != CIO && !proj) || y.c != CIO || x.n != y.n ||

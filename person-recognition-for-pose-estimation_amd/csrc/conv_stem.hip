@@ -232,6 +232,12 @@ extern "C" int prpe_stem_maxpool(const prpe_stem_desc* d, void* stream) {
     return PRPE_EINVAL;
   const int64_t fb = (int64_t)(d->h + 6) * d->xsh * 4;
   if (fb >= (1LL << 31)) return PRPE_EINVAL;
+  {                                                      // not in place (prpe.h)
+    uintptr_t ylo, yhi;
+    view_span(y, ylo, yhi);
+    const uintptr_t xlo = (uintptr_t)d->x, xhi = xlo + (uintptr_t)((d->n - 1) * d->xsn * 4 + fb);
+    if (spans_overlap(xlo, xhi, ylo, yhi)) return PRPE_EINVAL;
+  }
   StemK kp{};
   kp.x = d->x; kp.xsn = d->xsn; kp.xsh = d->xsh; kp.xframe_bytes = (int)fb;
   kp.x_amax = d->x_amax;

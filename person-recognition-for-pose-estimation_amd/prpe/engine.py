@@ -164,6 +164,10 @@ class Engine:
             ci, off = ci + 1, 0
         if ci == len(chunks):
             chunks.append(torch.zeros(max(AMAX_CHUNK, n), device=self.device, dtype=torch.float32))
+        elif chunks[ci].numel() - off < n:
+            # a chunk made for a smaller batch (chunks past the cursor are not handed out in this
+            # scope yet): a bigger one takes its place, zeroed like every chunk of the pool
+            chunks[ci] = torch.zeros(max(AMAX_CHUNK, n), device=self.device, dtype=torch.float32)
         t = chunks[ci][off:off + n]
         pool[1], pool[2] = ci, off + n
         return t
@@ -723,15 +727,18 @@ class Engine:
     def prepare(self, tasks=arch.TASKS):
         """Build every weight pack once (so timed regions contain kernels only)."""
         x = torch.zeros(1, 3, 64, 64, device=self.device)
+        # the heads run on this trunk output (its max|x| slots tagged), so every conv takes the
+        # precision it takes in a real forward -- the adapters' .0 GEMMs precision 3 (feat_prec) --
+        # and every fp16 weight plane is built here, not lazily inside a timed forward (the
+        # adapters upsample to fixed sizes, so a 2x2 feature map exercises the same packs)
         feat = self.trunk(x)
-        featb = self.empty(1, 20, 20, 2048).zero_()
         if "face_detection" in tasks:
-            self.yolo("yolo_face", featb)
+            self.yolo("yolo_face", feat)
         if "person_detection" in tasks:
-            self.yolo("yolo_person", featb)
+            self.yolo("yolo_person", feat)
         if "face_recognition" in tasks:
-            self.adaface(featb)
+            self.adaface(feat)
         if "pose_estimation" in tasks:
-            self.vitpose(featb)
+            self.vitpose(feat)
         del feat
         torch.cuda.synchronize(self.device)

@@ -46,6 +46,16 @@ def nhwc(t: torch.Tensor) -> torch.Tensor:
     return t.permute(0, 2, 3, 1)
 
 
+def _check_slots(what, n, *slots):
+    """max|x| / max|y| slot arrays: contiguous float32 device tensors of at least n (frames)
+    entries -- the kernels index them by frame, so a short array would be read or raised out of
+    bounds on the device."""
+    for a in slots:
+        if a is not None and (not isinstance(a, torch.Tensor) or a.dtype != torch.float32 or not a.is_cuda or
+                              a.numel() < n or not a.is_contiguous()):
+            raise ValueError(f"{what}: max|x| slots must be a contiguous float32 device [N >= {n}]")
+
+
 def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, tile=0, x_amax=None,
            y_amax=None, x2=None, x2_amax=None, x_planes=False, y_planes=False, w2=None, y2=None, w3=None,
            scale2=None, bias2=None, act2="none"):
@@ -56,10 +66,7 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
     tensor the kernel raises to max|y[n]| per frame (zero it first)."""
     d = ConvDesc()
     _gpu(pack.w_hi)
-    N = x.shape[0]
-    for a in (x_amax, y_amax, x2_amax):
-        if a is not None and (a.dtype != torch.float32 or not a.is_cuda or a.numel() < N or not a.is_contiguous()):
-            raise ValueError(f"prpe_conv2d[{pack.name}]: max|x| slots must be a contiguous float32 device [N]")
+    _check_slots(f"prpe_conv2d[{pack.name}]", x.shape[0], x_amax, y_amax, x2_amax)
     if precision == 3:
         h16, l16, s16 = pack.f16_planes()
         d.w_h16, d.w_l16, d.scale16 = h16.data_ptr(), l16.data_ptr(), s16.data_ptr()
@@ -113,6 +120,9 @@ def bottleneck(x, packs, y, x_amax, y_amax=None):
     y = relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1 x))))))) + x); ``packs`` = the three
     ConvPacks (BN folded, conv2 chunk-major), x_amax [N] per-frame max|x|, y_amax [N] raised."""
     _gpu(x, y, x_amax)
+    if x_amax is None:
+        raise ValueError("prpe_bottleneck: x_amax (per-frame max|x| of the block input) is required")
+    _check_slots("prpe_bottleneck", x.shape[0], x_amax, y_amax)
     d = BneckDesc()
     d.x, d.y = view(x), view(y)
     d.x_amax, d.y_amax = x_amax.data_ptr(), _ptr(y_amax)
@@ -136,6 +146,9 @@ def stem_maxpool(buf, h, w, x_amax, pack, y, y_amax=None):
     _gpu(buf, y, x_amax)
     if not buf.is_contiguous() or buf.dim() != 4 or buf.shape[3] != 4:
         raise PrpeError("stem_maxpool: buf must be a contiguous [N, H+6, W+8, 4] buffer")
+    if x_amax is None:
+        raise ValueError("prpe_stem_maxpool: x_amax (per-frame max|x| of the frames) is required")
+    _check_slots("prpe_stem_maxpool", buf.shape[0], x_amax, y_amax)
     d = StemDesc()
     d.x, d.xsn, d.xsh = buf.data_ptr(), buf.stride(0), buf.stride(1)
     d.n, d.h, d.w = buf.shape[0], h, w

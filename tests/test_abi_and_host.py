@@ -53,6 +53,42 @@ def test_invalid_arguments_are_rejected_before_launch():
     assert L.prpe_conv2d(C.byref(d), None) == -22
 
 
+def test_fused_launches_refuse_in_place_and_short_slots():
+    """prpe_bottleneck / prpe_stem_maxpool read x's halo and residual while other tiles write y:
+    an overlapping y is refused before launch (include/prpe.h); the Python wrappers check the
+    max|x| slot arrays like prpe_conv2d's (a short array would be indexed out of bounds)."""
+    L = _lib.lib()
+    x = _lib.View(0x100000, 2, 16, 16, 256, 16 * 16 * 256, 16 * 256, 256, 1)
+    d = _lib.BneckDesc(x=x, y=x, x_amax=0x1000, mid=64)
+    for i, k in enumerate((256, 576, 64)):
+        d.w_h16[i] = d.w_l16[i] = d.scale16[i] = d.bias[i] = 0x1000
+        d.k_pad[i] = k
+    assert L.prpe_bottleneck(C.byref(d), None) == -22                       # y == x
+    d.y = _lib.View(0x100000 + 4096, 2, 16, 16, 256, 16 * 16 * 256, 16 * 256, 256, 1)
+    assert L.prpe_bottleneck(C.byref(d), None) == -22                       # y overlaps x
+    st = _lib.StemDesc(x=0x100000, xsn=70 * 72 * 4, xsh=72 * 4, n=2, h=64, w=64, x_amax=0x1000, w_h16=0x1000,
+                       w_l16=0x1000, k_pad=224, scale16=0x1000, bias=0x1000,
+                       y=_lib.View(0x100000 + 64, 2, 16, 16, 64, 16 * 16 * 64, 16 * 64, 64, 1))
+    assert L.prpe_stem_maxpool(C.byref(st), None) == -22                    # y inside the frames
+    from prpe import ops
+    with pytest.raises(ValueError, match="slots"):
+        ops._check_slots("t", 4, torch.zeros(3))                           # short (and host) array
+
+
+def test_amax_slot_pool_grows_for_larger_batches():
+    """Engine.amax_slot: chunks made for a small batch are replaced when a later scope asks for
+    more slots than they hold (e.g. tokens of a bigger ViT batch), never sliced short."""
+    from prpe import engine as E
+    e = E.Engine({}, device="cpu")
+    for n in (64, 70000, 5, 200000, 3):
+        e._amax_begin("vit")
+        a = e.amax_slot(n)
+        b = e.amax_slot(n)
+        assert a.numel() == n and b.numel() == n and float(a.abs().sum() + b.abs().sum()) == 0.0
+        a.fill_(1.0)
+        b.fill_(2.0)
+
+
 def test_library_refuses_other_sources(monkeypatch):
     """lib() compares the source hash compiled into libprpe.so (build.py) with the hash of the
     sources beside it and refuses a library built from other sources."""

@@ -102,7 +102,12 @@ def test_config2_yolo_face_bs64(model, state_dict):
     from test_gpu_model import nms_match_rate
     rates = [nms_match_rate(dets[f, :cnt[f]], r) for f, r in zip(idx, R.non_max_suppression(ref))]
     print("config 2 end-to-end NMS match rate vs the oracle's detections:", rates)
-    assert min(rates) == 1.0      # measured on the committed tree (round 3)
+    # end to end, NMS runs on OUR scores, which differ from the oracle's by up to ~3e-5 (measured):
+    # a pair whose suppression decision is tied to that level (IoU within rounding of 0.65, or two
+    # scores that swap order) may legitimately flip, so a few of up to 300 kept rows per frame may
+    # differ without any regression (the bit-exact NMS check on the same tensor is the loop above).
+    # Measured 1.0 on every frame in rounds 3-4.
+    assert min(rates) >= 0.98
 
 
 def test_config3_vitpose_from_pixels_vs_transformers_golden(model):
