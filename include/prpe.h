@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PRPE_ABI_VERSION 7
+#define PRPE_ABI_VERSION 8
 
 /* activations (epilogues/prologues) */
 enum prpe_act {
@@ -89,6 +89,11 @@ typedef struct prpe_conv_desc {
                                  per operand: below fp32 accumulation error for K >= 64);
                                  needs w_h16/w_l16/scale16/x_amax, no in_scale, and a
                                  channel-chunked input (Ci % 32 == 0, k_order 1 or 1x1);
+                             4 = ONE fp16 plane per operand with the same power-of-2 scaling,
+                                 RNE, 1 term (~2^-12 per operand); needs w_h16/scale16/x_amax
+                                 (w_l16 unused), a channel-chunked input, no dual input / planes;
+                                 in_scale allowed (the kernel bounds max|PRO(x)| by
+                                 x_amax max|in_scale| + max|in_bias|); the AdaFace branch's policy;
                              1 = plain bf16 (1 term; diagnostics only) */
   int32_t tile;           /* 0 = auto; 1..6 = 128x128, 128x64, 128x32, 128x16, 256x128, 256x64
                              (register-staged); 10..12 LDS-DMA staged; 21..25 wave-row */
@@ -228,11 +233,14 @@ int prpe_stem_maxpool(const prpe_stem_desc* d, void* stream);
  * through it (x-interpolation, then y; kept for ablation). Both agree to fp32 rounding.
  * y_planes: write y in the planes format described at prpe_conv_desc: fused path, C % 8 == 0,
  * channel-contiguous, 32-B aligned; for a precision-0 consumer conv.
+ * y_amax (optional, ABI 8): device [N], y_amax[n] raised to max|y[n]| (zeroed by the caller;
+ * the per-frame bound a precision-3/4 consumer conv reads as its x_amax); fused path only.
  */
 int64_t prpe_upconv3x3_workspace_bytes(const prpe_view* z, const prpe_view* y);
 int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,
                    const float* scale, const float* bias, const float* slope, int32_t act,
-                   int32_t y_planes, void* workspace, int64_t workspace_bytes, void* stream);
+                   int32_t y_planes, float* y_amax, void* workspace, int64_t workspace_bytes,
+                   void* stream);
 
 /* Depthwise kxk conv (groups = C) + folded BN + act (+ post-act residual add when res.ptr).
  * Replaces yolopt Conv(g=ch) (nn.py:108, :248-250). */

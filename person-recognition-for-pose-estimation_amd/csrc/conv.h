@@ -109,6 +109,35 @@ __device__ __forceinline__ void split_planes_f16(f4 v, float sa, unsigned long l
   for (int q = 0; q < 2; ++q) pl[q] = (unsigned long long)u[q][0] | ((unsigned long long)u[q][1] << 32);
 }
 
+// precision 4: fp32 x8 -> ONE fp16 plane of v * sa (RNE, v_cvt_pk_f16_f32), one MFMA per
+// product. |v sa| < 2^15 by the choice of sa (as precision 3); operand error 2^-12 relative.
+__device__ __forceinline__ f16x8 cvt_f16_one(f4 v0, f4 v1, float sa) {
+  typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+  const h2v a = __builtin_convertvector(f2v{v0[0] * sa, v0[1] * sa}, h2v);
+  const h2v b = __builtin_convertvector(f2v{v0[2] * sa, v0[3] * sa}, h2v);
+  const h2v c = __builtin_convertvector(f2v{v1[0] * sa, v1[1] * sa}, h2v);
+  const h2v d = __builtin_convertvector(f2v{v1[2] * sa, v1[3] * sa}, h2v);
+  return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
+
+// precision 4 with an input-side affine (IR-50 pre-BN prologue): an upper bound of
+// max|s x + b| over the frame = amax(x) max|s| + max|b|, with max|s| and max|b| over the Ci
+// prologue channels reduced here (every lane gets the wave's maxima). A loose bound only costs
+// low-order bits of the scaled operand, never range.
+__device__ __forceinline__ void prologue_bounds(const float* s, const float* b, int ci, float& ms, float& mb) {
+  ms = 0.f;
+  mb = 0.f;
+  for (int c = threadIdx.x & 63; c < ci; c += 64) {
+    ms = fmaxf(ms, fabsf(s[c]));
+    mb = fmaxf(mb, fabsf(b[c]));
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    ms = fmaxf(ms, __shfl_xor(ms, o, 64));
+    mb = fmaxf(mb, __shfl_xor(mb, o, 64));
+  }
+}
+
 typedef __attribute__((address_space(1))) void* gbl_ptr_t;
 
 // one LDS-DMA piece: 16 B per lane from src (per lane) to dst_lds + 16 * lane (dst wave-uniform)
@@ -148,7 +177,7 @@ bool conv_wave_eligible(const ConvK& kp, int prec, int km);
 int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 
 // haloed-tile 3x3 kernel (conv_halo.hip): 3x3 / s1 / p1, chunk-major weights, precision 0
-// (fp32 or planes input) or 3; tile 30 = auto, 31..35 force a configuration.
+// (fp32 or planes input), 3 or 4; tile 30 = auto, 31..35 force a configuration.
 bool conv_halo_eligible(const ConvK& kp, int prec, int km);
 bool conv_halo_auto(const ConvK& kp, int prec);   // the automatic choice's shape rule
 

@@ -34,8 +34,7 @@
 // s ^ swz_rows(q): conv.h);
 // the W1 / W2 ring [4 stages][2 planes][64 rows][64 B] right after it (three K-steps of
 // lookahead; the block A operand of phase 1 is loaded two K-steps ahead into registers); phase
-// 3's W3 half [2 K-steps][2 planes][128 rows][64 B] overlays TT's last 16 KB and ring stages 0-1;
-// ring stage 3 holds conv3's scale / bias in phase 3 (round 4: read from LDS by the epilogue).
+// 3's W3 half [2 K-steps][2 planes][128 rows][64 B] overlays TT's last 16 KB and ring stages 0-1.
 #include "conv.h"
 
 namespace prpe_k {
@@ -140,8 +139,6 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void b
   using S = BShape<MIDT, PROJ>;
   constexpr int MID = S::MID, CIO = S::CIO, CIN = S::CIN, NK1 = S::NK1, R3 = S::R3, W3_STEP = S::W3_STEP;
   constexpr int STAGE = S::STAGE, PPW = S::PPW, RING_OFF = S::RING_OFF, W3_OFF = S::W3_OFF;
-  constexpr int SB3_OFF = RING_OFF + 3 * STAGE;              // phase 3: conv3 scale / bias
-  static_assert(2 * CIO * 4 <= STAGE && W3_OFF + (S::W3DB ? 2 : 1) * W3_PART <= RING_OFF + 2 * STAGE, "SB3");
   constexpr int NJ1 = MID / 16;                              // 16-channel column blocks of t1 / t2
   __shared__ __attribute__((aligned(1024))) unsigned char lds[S::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -402,19 +399,6 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void b
       bl_lds16(q ? wr[2][1] : wr[2][0], w3b + ks * W3_STEP + (q * R3 + rb * 16) * 64, vo, ks * BK_ * 2);
     }
   };
-  // conv3's scale / bias (CIO floats each) into ring stage 3 (free since the barrier above) by
-  // LDS-DMA, older than every phase-3 access the counted waits below count: the epilogue reads
-  // them from LDS. Loaded into registers there (round 3), they were the youngest vector-memory
-  // ops at each use, so the compiler's wait for them (vmcnt(0), in-order counter) also drained
-  // the part's previous y stores: store -> load -> wait -> store, serialised per 16 columns.
-  {
-    constexpr int NSB = CIO / 256;                           // 1-KiB pieces per array
-    if (wave < 2 * NSB) {
-      const int arr = wave / NSB, pc = wave % NSB;
-      bl_lds16(buf_rsrc(arr ? p.bi[2] : p.sc[2], CIO * 4), lds + SB3_OFF + (arr * CIO + pc * 256) * 4,
-               (unsigned)(pc * 1024 + lane * 16), 0);
-    }
-  }
   issue_w3(0);
   __syncthreads();
   m2 = wmax2[0];
@@ -513,8 +497,7 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void b
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c0 = h * R3 + j * 16 + fg * 4;
-      const float* const sb3 = reinterpret_cast<const float*>(lds + SB3_OFF);
-      const f4 s = *reinterpret_cast<const f4*>(sb3 + c0), b = *reinterpret_cast<const f4*>(sb3 + CIO + c0);
+      const f4 s = *reinterpret_cast<const f4*>(p.sc[2] + c0), b = *reinterpret_cast<const f4*>(p.bi[2] + c0);
       f4 v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {

@@ -84,15 +84,18 @@ __device__ __forceinline__ void stage_planes(const float* w, int rows, int cols,
 // [nmid <= 64][Co] first, back into the slice, then z = z1 w3^T (see prpe.h, w2 / w3).
 // WN: waves along N (WN = 2: a 2 x 2 wave grid, wave tile 64 px x BN/2; the B fragments of a
 // K-step are read by 2 waves instead of 4: -20 % LDS reads per MFMA at 4 waves).
-template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0, int WN = 1>
+// ONE (precision 4, with F16): one scaled fp16 plane per operand (RNE), one MFMA per product;
+// the B ring stages the weights' hi plane only.
+template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0, int WN = 1, bool ONE = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void conv_halo_kernel(ConvK p, int tiles_w, int tiles_h) {
   static_assert(TC % 16 == 0 && (TR * TC / 16) % (NW / WN) == 0 && TN % WN == 0, "tile");
   static_assert(!(F16 && APL), "planes input is precision 0");
+  static_assert(!ONE || (F16 && TAPS == 0), "single fp16 plane: precision 4, no epilogue GEMM");
   static_assert(WN == 1 || WN == 2, "waves along N");
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
   constexpr int TM = TR * TC / 16 / (NW / WN);          // 16-pixel row blocks per wave
   constexpr int TNW = TN / WN;                          // 16-column tiles per wave
-  constexpr int BN = TN * 16, NP = 2;
+  constexpr int BN = TN * 16, NP = ONE ? 1 : 2;
   constexpr int HW_ = TC + 2, HP = (TR + 2) * HW_;      // halo pixels
   constexpr int HQ = (HP + 7) / 8;                      // 1-KiB DMA pieces per halo
   constexpr int HALO = HQ * 8 * 128;                    // bytes per halo buffer
@@ -241,6 +244,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         if constexpr (APL) {
           af[0][i] = __builtin_bit_cast(bf16x8, v0);
           af[1][i] = __builtin_bit_cast(bf16x8, v1);
+        } else if constexpr (ONE) {
+          af[0][i] = cvt_f16_one(v0, v1, sa);
         } else if constexpr (F16) {
           unsigned long long p0[2], p1[2];
           split_planes_f16(v0, sa, p0);
@@ -337,7 +342,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
           res[e] = *reinterpret_cast<const f4*>(p.r + (int64_t)n * p.rsn + (int64_t)oh * p.rsh + (int64_t)ow * p.rsw + col);
       }
     }
-#pragma unroll
+    // (ONE: two rows at a time; the fully unrolled form, with every activation's code inlined,
+    // spilled ~340 VGPRs in this variant)
+#pragma unroll(ONE ? 2 : EB)
     for (int e = 0; e < EB; ++e) {
       f4 v = *reinterpret_cast<const f4*>(ct + (rr0 + RPP * e) * CS + cc * 4);
       if (!ok[e]) continue;
@@ -425,7 +432,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   if (p.y_amax) amax_commit(p.y_amax + n, ym);
 }
 
-template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0, int WN = 1>
+template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0, int WN = 1, bool ONE = false>
 int launch_halo(const ConvK& kp0, hipStream_t st) {
   ConvK kp = kp0;
   if (kp.w2 && kp.Co > TN * 16) return PRPE_EINVAL;     // the tap GEMM needs every column in one tile
@@ -434,14 +441,17 @@ int launch_halo(const ConvK& kp0, hipStream_t st) {
   const int64_t nwg = (int64_t)(kp.M / kp.HoWo) * tiles_h * tiles_w * kp.tiles_n;
   if (nwg <= 0 || nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
-  hipLaunchKernelGGL((conv_halo_kernel<NW, TR, TC, TN, F16, APL, TAPS, WN>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp,
-                     tiles_w, tiles_h);
+  hipLaunchKernelGGL((conv_halo_kernel<NW, TR, TC, TN, F16, APL, TAPS, WN, ONE>), dim3(kp.nwg), dim3(NW * 64), 0, st,
+                     kp, tiles_w, tiles_h);
   return launch_status();
 }
 
 template <int NW, int TR, int TC, int TN, int WN = 1>
 int launch_halo_kind(const ConvK& kp, int prec, hipStream_t st) {
   if (prec == 3) return launch_halo<NW, TR, TC, TN, true, false, 0, WN>(kp, st);
+  if constexpr ((TN * 16 / 16) % NW == 0)             // single-plane B ring: whole pieces per wave
+    if (prec == 4) return launch_halo<NW, TR, TC, TN, true, false, 0, WN, true>(kp, st);
+  if (prec == 4) return PRPE_EINVAL;
   return kp.x_planes ? launch_halo<NW, TR, TC, TN, false, true, 0, WN>(kp, st)
                      : launch_halo<NW, TR, TC, TN, false, false, 0, WN>(kp, st);
 }
@@ -450,6 +460,7 @@ int launch_halo_kind(const ConvK& kp, int prec, hipStream_t st) {
 template <int TAPS, int WN, int NW = 4>
 int launch_halo_taps_t(const ConvK& kp, int prec, hipStream_t st) {
   constexpr int TR = NW == 4 ? 8 : 16;
+  if (prec == 4) return PRPE_EINVAL;
   if (prec == 3) return launch_halo<NW, TR, 16, 8, true, false, TAPS, WN>(kp, st);
   return kp.x_planes ? launch_halo<NW, TR, 16, 8, false, true, TAPS, WN>(kp, st)
                      : launch_halo<NW, TR, 16, 8, false, false, TAPS, WN>(kp, st);
@@ -477,11 +488,12 @@ bool conv_halo_eligible(const ConvK& kp, int prec, int km) {
   // 3x3 / stride 1 / pad 1 over whole 32-channel chunks (chunk-major weights), vectorised
   // epilogue, precision 0 (fp32 or planes input) or 3 (fp16 planes + the input's max bound)
   const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.x_planes;
+  const bool p4 = prec == 4 && kp.wh16 && kp.x_amax && !kp.x_planes;
   // buffer descriptors: one frame of x and one weight plane each < 2^31 bytes (32-bit offsets)
   const int64_t frame_bytes = ((int64_t)(kp.Hi - 1) * kp.xsh + (int64_t)(kp.Wi - 1) * kp.xsw + kp.Ci) * 4;
   const int64_t w_bytes = (int64_t)kp.k_pad * 2 * (((kp.Co + 127) / 128) * 128);
   return km == 2 && kp.KH == 3 && kp.KW == 3 && kp.stride == 1 && kp.pad == 1 && kp.Ci % HBK == 0 &&
-         kp.vec_out && (prec == 0 || p3) && !kp.in_scale && !kp.x2 && kp.k_pad == kp.K && kp.zero &&
+         kp.vec_out && (prec == 0 || p3 || p4) && !kp.in_scale && !kp.x2 && kp.k_pad == kp.K && kp.zero &&
          kp.Hi == kp.Ho && kp.Wi == kp.Wo && kp.xsh >= 0 && kp.xsw >= 0 && frame_bytes < (1LL << 31) &&
          w_bytes < (1LL << 31);
 }

@@ -564,10 +564,14 @@ int launch_cfg(const ConvK& kp0, int km, int prec, hipStream_t st) {
 // 2 chunk-major).
 static int conv_setup(const prpe_conv_desc* d, ConvK& kp, int& km) {
   if (!d || !view_ok(&d->x) || !view_ok(&d->y) || !d->w_hi) return PRPE_EINVAL;
-  if (d->precision < 0 || d->precision > 3) return PRPE_EINVAL;
+  if (d->precision < 0 || d->precision > 4) return PRPE_EINVAL;
   if ((d->precision == 0 || d->precision == 2) && !d->w_lo) return PRPE_EINVAL;
   if (d->precision == 2 && !d->w_lo2) return PRPE_EINVAL;
   if (d->precision == 3 && (!d->w_h16 || !d->w_l16 || !d->scale16 || !d->x_amax || d->in_scale))
+    return PRPE_EINVAL;
+  // precision 4: one fp16 plane (w_h16) and the input's per-frame max bound; a prologue affine is
+  // allowed (its output is bounded in-kernel); no dual input, no planes format
+  if (d->precision == 4 && (!d->w_h16 || !d->scale16 || !d->x_amax || d->x2.ptr || d->x_planes || d->y_planes))
     return PRPE_EINVAL;
   if (d->kh <= 0 || d->kw <= 0 || d->stride <= 0 || d->pad < 0) return PRPE_EINVAL;
   const prpe_view& x = d->x; const prpe_view& y = d->y;
@@ -636,7 +640,7 @@ static int conv_setup(const prpe_conv_desc* d, ConvK& kp, int& km) {
   if (d->y_planes && (y.sc != 1 || y.c % 8 || y.sw % 8 || y.sh % 8 || y.sn % 8 || (uintptr_t)y.ptr % 32 ||
                       d->precision == 1))
     return PRPE_EINVAL;
-  if (d->precision == 3) kp.scale = d->scale16;
+  if (d->precision >= 3) kp.scale = d->scale16;
   // epilogue 1x1 GEMM (haloed-tile 3x3 kernel only)
   if (d->w2 && d->tile != 0 && (d->tile < 30 || d->tile >= 40)) return PRPE_EINVAL;
   if (d->w2) {
@@ -763,8 +767,8 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;
   if (tile == 0 && halo_on && conv_halo_auto(kp, prec) && conv_halo_eligible(kp, prec, km))
     return conv_halo_launch(kp, prec, 30, st);
-  // precision 3 (split fp16) is implemented by the wave-row kernel only
-  if (prec == 3) {
+  // precision 3 (split fp16) and 4 (one fp16 plane) are implemented by the wave-row kernel only
+  if (prec >= 3) {
     if (tile != 0 && tile < 20) return PRPE_EINVAL;
     return conv_wave_eligible(kp, prec, km) ? conv_wave_launch(kp, prec, tile ? tile : 20, st) : PRPE_EINVAL;
   }

@@ -49,16 +49,22 @@ constexpr int BK = 32;
 // output's pixel grid, e.g. a stride-2 subsampling of the block input).
 // APL: the input tensor is stored as interleaved bf16 planes (see prpe.h, "planes format"):
 // the 32 bytes a lane loads for 8 channels already are the hi and lo fragments, no split.
+// ONE (precision 4, with F16): ONE scaled fp16 plane per operand (RNE), one MFMA per product
+// instead of three; the weights' hi plane alone (w_h16 = RNE(w 2^e[co])) is staged. Allows the
+// prologue affine: the activation scale then comes from a bound of the prologue's output
+// (prologue_bounds, conv.h).
 template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false,
-          bool APL = false>
+          bool APL = false, bool ONE = false>
 __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   static_assert(!APL || (NP == 2 && !F16 && !PRO && !DUAL), "planes input: two bf16 planes only");
-  static_assert(!F16 || (NP == 2 && !PRO), "f16 planes: two planes, no prologue");
+  static_assert(!F16 || (NP == 2 && (!PRO || ONE)), "f16 planes: two planes, no prologue unless single-plane");
+  static_assert(!ONE || (F16 && !DUAL && !APL), "single fp16 plane: precision 4");
   static_assert(!DUAL || !PRO, "dual input: no prologue");
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
+  constexpr int NPL = ONE ? 1 : NP;                   // planes staged and multiplied
   constexpr int WTM = TM * 16, BM = NW * WTM, BN = TN * 16;
-  constexpr int B_STAGE = NP * BN * 64;               // bf16 [NP][BN][32]
-  constexpr int NB_TOT = NP * BN / 16;                // 1-KiB LDS-DMA pieces per stage
+  constexpr int B_STAGE = NPL * BN * 64;              // bf16 / f16 [NPL][BN][32]
+  constexpr int NB_TOT = NPL * BN / 16;               // 1-KiB LDS-DMA pieces per stage
   constexpr int IB = (NB_TOT + NW - 1) / NW;          // per wave (surplus slots repeat a piece)
   constexpr int CS = BN + 4;                          // epilogue row pitch (floats)
   constexpr int EPI = NW * 16 * CS * 4;
@@ -92,10 +98,14 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   const int nb = (nf0 + 1) * p.HoWo;
   const bool two = p.HoWo >= WTM;
   float am0 = 0.f, am1 = 0.f;                         // max|x| of frames nf0, nf0 + 1 (F16)
+  // PRO (precision 4 only): max|in_scale x + in_bias| <= max|x| pS + pB
+  float pS = 1.f, pB = 0.f;
+  if constexpr (F16 && PRO) prologue_bounds(p.in_scale, p.in_bias, p.Ci, pS, pB);
+  auto bound = [&](float am) { return PRO ? am * pS + pB : am; };
   if constexpr (F16) {
     if (two) {
-      if (wrow0 < p.M) am0 = DUAL ? fmaxf(p.x_amax[nf0], p.x2_amax[nf0]) : p.x_amax[nf0];
-      if (nb < p.M) am1 = DUAL ? fmaxf(p.x_amax[nf0 + 1], p.x2_amax[nf0 + 1]) : p.x_amax[nf0 + 1];
+      if (wrow0 < p.M) am0 = bound(DUAL ? fmaxf(p.x_amax[nf0], p.x2_amax[nf0]) : p.x_amax[nf0]);
+      if (nb < p.M) am1 = bound(DUAL ? fmaxf(p.x_amax[nf0 + 1], p.x2_amax[nf0 + 1]) : p.x_amax[nf0 + 1]);
     }
   }
   const __amdgpu_buffer_rsrc_t xr =
@@ -114,7 +124,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
         // activation scale of this row's frame: max|x| < 2^e -> 2^(15 - e); a dual GEMM's two
         // inputs share one scale (their per-frame maxima combined)
         const float am = two ? (m >= nb ? am1 : am0)
-                             : (DUAL ? fmaxf(p.x_amax[n], p.x2_amax[n]) : p.x_amax[n]);
+                             : bound(DUAL ? fmaxf(p.x_amax[n], p.x2_amax[n]) : p.x_amax[n]);
         sa[i] = ldexpf(1.f, 15 - f16_scale_exp(am));
       }
       const int rem = m - n * p.HoWo;
@@ -152,16 +162,16 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     bdst[i] = (q * BN + rb * 16) * 64;
     bq[i] = q;                                          // wave-uniform
   }
-  __amdgpu_buffer_rsrc_t wr[NP];
+  __amdgpu_buffer_rsrc_t wr[NPL];
 #pragma unroll
-  for (int q = 0; q < NP; ++q) wr[q] = buf_rsrc(planes[q], wbytes);
+  for (int q = 0; q < NPL; ++q) wr[q] = buf_rsrc(planes[q], wbytes);
   auto issue_b = [&](int kt, int stage) {
     unsigned char* sb = lds + stage * B_STAGE;
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       __amdgpu_buffer_rsrc_t r = wr[0];
 #pragma unroll
-      for (int q = 1; q < NP; ++q)
+      for (int q = 1; q < NPL; ++q)
         if (bq[i] == q) r = wr[q];
       bl_lds16(r, sb + bdst[i], bvo[i], kt * BK * 2);
     }
@@ -227,6 +237,8 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       if constexpr (APL) {
         af[0][i] = __builtin_bit_cast(bf16x8, v0);
         af[1][i] = __builtin_bit_cast(bf16x8, v1);
+      } else if constexpr (ONE) {
+        af[0][i] = cvt_f16_one(v0, v1, sa[i]);
       } else if constexpr (F16) {
         unsigned long long p0[2], p1[2];
         split_planes_f16(v0, sa[i], p0);
@@ -261,8 +273,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
       frag_t bfr[NP];
 #pragma unroll
-      for (int q = 0; q < NP; ++q) bfr[q] = *reinterpret_cast<const frag_t*>(bp + q * BN * 64);
+      for (int q = 0; q < NPL; ++q) bfr[q] = *reinterpret_cast<const frag_t*>(bp + q * BN * 64);
       // partial products smallest first; terms with plane-index sum >= NP are dropped
+      if constexpr (ONE) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[i][j] = mfma16(af[0][i], bfr[0], acc[i][j]);
+        continue;
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -371,7 +388,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
         if (two) {
           v = v * (fn[e] == nf0 ? inv0 : inv1);
         } else {                                      // frames smaller than a wave tile
-          const float am = DUAL ? fmaxf(p.x_amax[fn[e]], p.x2_amax[fn[e]]) : p.x_amax[fn[e]];
+          const float am = bound(DUAL ? fmaxf(p.x_amax[fn[e]], p.x2_amax[fn[e]]) : p.x_amax[fn[e]]);
           v = v * ldexpf(1.f, f16_scale_exp(am) - 15);
         }
       }
@@ -411,13 +428,23 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   }
 }
 
-template <int NW, int TM, int TN, int NP, int STAGES, bool F16 = false>
+template <int NW, int TM, int TN, int NP, int STAGES, bool F16 = false, bool ONE = false>
 int launch(const ConvK& kp0, hipStream_t st) {
   constexpr int BM = NW * TM * 16, BN = TN * 16;
   ConvK kp = kp0;
   const int tiles_m = (kp.M + BM - 1) / BM;
   kp.tiles_n = (kp.Co + BN - 1) / BN;
   kp.nwg = tiles_m * kp.tiles_n;
+  if constexpr (ONE) {
+    if (kp.x2 || kp.x_planes) return PRPE_EINVAL;
+    if (kp.in_scale)
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, true, true, false, false, true>), dim3(kp.nwg),
+                         dim3(NW * 64), 0, st, kp);
+    else
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, false, false, true>), dim3(kp.nwg),
+                         dim3(NW * 64), 0, st, kp);
+    return launch_status();
+  }
   if (kp.x2) {
     if constexpr (F16)
       hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
@@ -449,6 +476,7 @@ bool conv_wave_eligible(const ConvK& kp, int prec, int km) {
   // has no prologue
   const bool chunked = km == 2 || (km == 1 && kp.KH * kp.KW == 1 && kp.Ci % 32 == 0);
   const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.in_scale && (!kp.x2 || kp.x2_amax);
+  const bool p4 = prec == 4 && kp.wh16 && kp.x_amax && !kp.x2 && (!kp.in_scale || kp.in_bias);
   const bool planes_ok = !kp.x_planes || (prec == 0 && !kp.in_scale && !kp.x2);
   // buffer descriptors: a wave's rows (at most 64, spanning at most 64 / HoWo + 2 frames) and its
   // taps must lie within 2^31 bytes of the wave's first frame, with non-negative strides
@@ -459,7 +487,7 @@ bool conv_wave_eligible(const ConvK& kp, int prec, int km) {
   const bool addr_ok = kp.xsn >= 0 && kp.xsh >= 0 && kp.xsw >= 0 && x_span < 0x7FFFFFF0LL &&
                        (!kp.x2 || (kp.x2sn >= 0 && kp.x2sh >= 0 && kp.x2sw >= 0 && x2_span < 0x7FFFFFF0LL)) &&
                        (int64_t)kp.k_pad * 2 * kp.Co < (1LL << 30);
-  return chunked && kp.vec_out && (prec == 0 || prec == 2 || p3) && kp.K % BK == 0 && kp.k_pad == kp.K &&
+  return chunked && kp.vec_out && (prec == 0 || prec == 2 || p3 || p4) && kp.K % BK == 0 && kp.k_pad == kp.K &&
          kp.zero != nullptr && planes_ok && addr_ok;
 }
 
@@ -499,7 +527,7 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       return e ? atoi(e) : 27;
     }();
     if (prec == 0) tile = wide;
-    else if (prec == 3) tile = kp.Co > 64 && (kp.K > 128 || p3_smallk_wide) ? wide3 : p3_narrow;
+    else if (prec >= 3) tile = kp.Co > 64 && (kp.K > 128 || p3_smallk_wide) ? wide3 : p3_narrow;
     else tile = kp.Co > 64 && kp.K > 128 ? tile2 : 24;
   }
   if (prec == 0) {
@@ -525,6 +553,15 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       case 25: return launch<8, 2, 4, 2, 3, true>(kp, st);   // 256 x 64, wave 32 x 64
       case 26: return launch<4, 2, 8, 2, 3, true>(kp, st);   // 128 x 128, wave 32 x 128, 4 waves
       case 27: return launch<4, 2, 8, 2, 2, true>(kp, st);   // 128 x 128, 2 stages
+      default: return PRPE_EINVAL;
+    }
+  }
+  if (prec == 4) {                                     // the precision-3 shapes, one fp16 plane
+    switch (tile) {
+      case 24: return launch<4, 4, 8, 2, 3, true, true>(kp, st);
+      case 25: return launch<8, 2, 4, 2, 3, true, true>(kp, st);   // 256 x 64, wave 32 x 64
+      case 26: return launch<4, 2, 8, 2, 3, true, true>(kp, st);   // 128 x 128, 3 stages
+      case 27: return launch<4, 2, 8, 2, 2, true, true>(kp, st);   // 128 x 128, 2 stages
       default: return PRPE_EINVAL;
     }
   }

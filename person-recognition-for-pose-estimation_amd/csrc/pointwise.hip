@@ -63,6 +63,7 @@ struct UpK {
   int chunks;     // ceil(per_row / 256)
   int y_planes;   // write y in the planes format (include/prpe.h, prpe_conv_desc)
   int xcd;        // fused kernel: XCD-contiguous block order
+  float* y_amax;  // optional per-frame max|y| slots (a block covers one frame)
 };
 
 // Fused one-pass form (no workspace). One thread = VW channels of one output column, for a
@@ -133,7 +134,9 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
     tly[t] = ly;
   }
   __syncthreads();
-  if (j >= p.per_row) return;
+  // lanes past the row stay for the block's max|y| reduction (amax_commit) but do no work
+  const bool jl = j < p.per_row;
+  if (!jl && !p.y_amax) return;
   const int cgroups = p.Co / VW;
   const int ox = j / cgroups, c0 = (j - ox * cgroups) * VW;
   const int zsw = (int)p.z.sw, zsc = (int)p.z.sc;
@@ -166,7 +169,8 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
   const int yo = ox * (int)p.y.sw + c0 * (int)p.y.sc;                    // per thread
   float hA[3][VW], hB[3][VW];
   int cur[3] = {-2, -2, -2};
-  for (int oy = oy0; oy < oy1; ++oy) {
+  float ym = 0.f;
+  for (int oy = oy0; oy < (jl ? oy1 : oy0); ++oy) {
     float acc[VW];
 #pragma unroll
     for (int v = 0; v < VW; ++v) acc[v] = 0.f;
@@ -212,6 +216,8 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
 #pragma unroll
       for (int v = 0; v < VW; ++v) out[v] = apply_act(acc[v] * sc[v] + bi[v], ACT >= 0 ? ACT : p.act, sl[v]);
     }
+#pragma unroll
+    for (int v = 0; v < VW; ++v) ym = fmaxf(ym, fabsf(out[v]));
     float* y = yn + (int64_t)oy * p.y.sh + yo;
     if constexpr ((ABL & 2) != 0) {
       if (out[0] + out[VW - 1] == 12345.678f) y[0] = out[0];
@@ -233,6 +239,7 @@ __global__ __launch_bounds__(256) void upconv_fused_kernel(UpK p, int R, int rbl
 #pragma unroll
     for (int v = 0; v < VW; ++v) y[(int64_t)v * p.y.sc] = out[v];
   }
+  if (p.y_amax) amax_commit(p.y_amax + n, ym);
 }
 
 // LDS-DMA form (round 3; the automatic choice for VW = 4 whenever its geometry rules hold). Why:
@@ -381,6 +388,7 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
   float* yn = p.y.ptr + (int64_t)n * p.y.sn;
   float hA[3][4], hB[3][4];
   int cur[3] = {-2, -2, -2};
+  float ym = 0.f;
   for (int oy = oy0; oy < oy1; ++oy) {
     const int need = __builtin_amdgcn_readfirstlane(hi_at(oy));
     if (need > in_use) {
@@ -420,6 +428,7 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
     for (int v = 0; v < 4; ++v) pre[v] = acc[v] * sc[v] + bi[v];
     const f32x4 o4 = apply_act4(pre, ACT >= 0 ? ACT : p.act, f32x4{sl[0], sl[1], sl[2], sl[3]});
     const float out[4] = {o4[0], o4[1], o4[2], o4[3]};
+    ym = fmaxf(ym, amax4(o4));
     float* y = yn + (int64_t)oy * p.y.sh + yo;
     if constexpr (PL)
       store_planes4<true>(reinterpret_cast<uint16_t*>(y - (c0 + cg * 4)), c0 + cg * 4,
@@ -427,6 +436,7 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
     else
       __builtin_nontemporal_store(f32x4{out[0], out[1], out[2], out[3]}, reinterpret_cast<f32x4*>(y));
   }
+  if (p.y_amax) amax_commit(p.y_amax + n, ym);
 }
 
 // Separable form of the same sum (6 loads per output instead of 36):
@@ -925,13 +935,16 @@ static bool upd_geometry_ok(const prpe_view* z, const prpe_view* y, int ac) {
 
 extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners,
                               const float* scale, const float* bias, const float* slope, int32_t act,
-                              int32_t y_planes, void* workspace, int64_t workspace_bytes, void* stream) {
+                              int32_t y_planes, float* y_amax, void* workspace, int64_t workspace_bytes,
+                              void* stream) {
   if (!view_ok(z) || !view_ok(y) || z->n != y->n || z->c != 9 * y->c) return PRPE_EINVAL;
+  if (y_amax && workspace) return PRPE_EINVAL;        // max|y| on the one-pass kernels only
   if (act == PRPE_ACT_PRELU && !slope) return PRPE_EINVAL;
   UpK p{};
   p.z = *z; p.y = *y; p.Co = y->c; p.ac = align_corners ? 1 : 0;
   p.scale = scale; p.bias = bias; p.slope = slope; p.act = act;
   p.y_planes = y_planes ? 1 : 0;
+  p.y_amax = y_amax;
   const bool v4 = (y->c % 4 == 0) && z->sc == 1 && (z->sw % 4 == 0) && (z->sh % 4 == 0) &&
                   (z->sn % 4 == 0) && ((uintptr_t)z->ptr % 16 == 0) &&
                   (y->sc != 1 || ((y->sw % 4 == 0) && (y->sh % 4 == 0) && (y->sn % 4 == 0) &&

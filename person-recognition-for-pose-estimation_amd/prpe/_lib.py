@@ -14,7 +14,7 @@ from ._srchash import source_hash
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libprpe.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 
 class PrpeError(RuntimeError):
@@ -72,7 +72,7 @@ SIGNATURES = {
     "prpe_bottleneck": (C.c_int, [C.POINTER(BneckDesc), _P]),
     "prpe_stem_maxpool": (C.c_int, [C.POINTER(StemDesc), _P]),
     "prpe_upconv3x3_workspace_bytes": (C.c_int64, [_VP, _VP]),
-    "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _I, _P, _L, _P]),
+    "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _I, _P, _P, _L, _P]),
     "prpe_dwconv": (C.c_int, [_VP, _VP, _VP, _P, _I, _I, _I, _P, _P, _I, _P]),
     "prpe_maxpool": (C.c_int, [_VP, _VP, _I, _I, _I, _P]),
     "prpe_upsample_nearest2x": (C.c_int, [_VP, _VP, _P]),

@@ -32,12 +32,17 @@ BN_EPS = 1e-5
 # Per-component conv precision (prpe_conv2d ``precision``): 2 = 3-plane bf16 split, exact fp32
 # operands (6 MFMA terms); 3 = 2-plane fp16 split with power-of-2 scaling (3 terms, ~2^-21 per
 # operand, below fp32's own accumulation error; needs a chunked input with a tracked max|x|,
-# else the conv runs precision 2); 0 = 2-plane bf16 split (3 terms, ~2^-17). "auto" keeps
-# fp32-faithful products where errors are amplified most (measured, DESIGN.md "Precision"):
-# the ResNet-50 trunk every head consumes, and the small YOLO net whose DFL box decode
-# multiplies logit errors by the stride; the large adapters and the ViT run the bf16 3-term
-# split.
-AUTO_POLICY = {"trunk": 3, "yolo_adapter": 0, "yolo_net": 2, "adaface": 0, "vit": 0}
+# else the conv runs precision 2); 0 = 2-plane bf16 split (3 terms, ~2^-17); 4 = ONE scaled
+# fp16 plane (1 term, ~2^-12 per operand; per-frame max|x| tracked through the component, else
+# the conv runs precision 0). "auto" keeps fp32-faithful products where errors are amplified
+# most (measured, DESIGN.md "Precision"): the ResNet-50 trunk every head consumes, and the small
+# YOLO net whose DFL box decode multiplies logit errors by the stride; the large adapters and
+# the ViT run the bf16 3-term split; the AdaFace branch (adapter + IR-50), whose embedding is
+# least sensitive to operand rounding (precision study: 1.8e-4 against the 1e-3 bar), runs one
+# fp16 term (round 4). PRPE_ADAFACE_PREC=0 restores the 3-term split there (A/B runs).
+AUTO_POLICY = {"trunk": 3, "yolo_adapter": 0, "yolo_net": 2, "vit": 0,
+               "adaface": int(os.environ.get("PRPE_ADAFACE_PREC", "4"))}
+F16_PRECS = (3, 4)                  # precisions that read / keep per-frame max|x| slots
 AMAX_CHUNK = 1 << 16                # floats per chunk of a component's max|y| slot pool
 # PRPE_PLANES=0 keeps every activation in fp32 (A/B runs of the planes-format handoff)
 PLANES_ON = os.environ.get("PRPE_PLANES", "1") != "0"
@@ -72,7 +77,7 @@ class _Prec:
     def __enter__(self):
         self.saved = (self.e.precision, self.e._amax_scope)
         self.e.precision = self.e.policy.get(self.c, self.saved[0])
-        if self.e.precision == 3:
+        if self.e.precision in F16_PRECS:
             self.e._amax_begin(self.c)
 
     def __exit__(self, *a):
@@ -179,9 +184,10 @@ class Engine:
                              all(st % 4 == 0 for st in t.stride()[:3]))
 
     @staticmethod
-    def _f16_ok(x, p: ConvPack, out, res=None):
+    def _f16_ok(x, p: ConvPack, out, res=None, prologue=False):
+        """``prologue``: an input-side affine is allowed (precision 4 bounds it in-kernel)."""
         chunked = p.k_order == 1 or (p.kh * p.kw == 1 and p.ci % 32 == 0)
-        return (chunked and p.in_scale is None and x.stride(3) == 1 and x.data_ptr() % 16 == 0 and
+        return (chunked and (prologue or p.in_scale is None) and x.stride(3) == 1 and x.data_ptr() % 16 == 0 and
                 Engine._vec4(out) and Engine._vec4(res) and getattr(x, "_prpe_amax", None) is not None)
 
     def pk_dual(self, q) -> ConvPack:
@@ -202,12 +208,14 @@ class Engine:
         return p
 
     def conv(self, x, p: ConvPack, out=None, res=None, res_mode=0, act=None, x2=None, x2_amax=None,
-             planes_out=False, w2=None, y2=None, prec=None, **stage2):
+             planes_out=False, w2=None, y2=None, prec=None, track=True, **stage2):
         """``x2``: second 1x1 input on the output grid (dual-input GEMM, see prpe.h).
         ``planes_out``: the only consumer is a precision-0 wave-row conv: write the planes format.
         ``w2``/``y2``: epilogue 1x1 GEMM into y2 (prpe.h); ``out`` is then not written;
         ``stage2``: its second stage (w3, scale2, bias2, act2; prpe.h).
-        ``prec``: this conv's precision instead of the component's (Engine.feat_prec)."""
+        ``prec``: this conv's precision instead of the component's (Engine.feat_prec).
+        ``track``: raise the output's per-frame max|y| slots in a precision-3/4 component (off for
+        an output no conv consumes, e.g. the IR-50 output layer's split-K GEMM)."""
         B, H, W, _ = x.shape
         Ho = (H + 2 * p.pad - p.kh) // p.stride + 1
         Wo = (W + 2 * p.pad - p.kw) // p.stride + 1
@@ -216,8 +224,10 @@ class Engine:
         prec = self.precision if prec is None else prec
         if prec == 3 and (not self._f16_ok(x, p, out, res) or (x2 is not None and x2_amax is None)):
             prec = 2
-        xa = getattr(x, "_prpe_amax", None) if prec == 3 else None
-        ya = self.amax_slot(B) if self.precision == 3 and w2 is None else None
+        if prec == 4 and (not self._f16_ok(x, p, out, res, prologue=True) or x2 is not None):
+            prec = 0
+        xa = getattr(x, "_prpe_amax", None) if prec in F16_PRECS else None
+        ya = self.amax_slot(B) if self.precision in F16_PRECS and w2 is None and track else None
         x_planes = getattr(x, "_prpe_planes", False)
         if x_planes and prec != 0:
             raise RuntimeError(f"{p.name}: planes-format input needs precision 0, got {prec}")
@@ -265,7 +275,11 @@ class Engine:
             out = self.empty(B, size[0], size[1], co)
         slope = self.dev(prelu) if prelu else None
         planes = PLANES_ON and planes and self.precision == 0 and co % 8 == 0 and out.is_contiguous()
-        ops.upconv3x3(z, out, align_corners, self._aux[key], self._aux[key + "b"], slope, act, y_planes=planes)
+        # a precision-3/4 consumer reads the output's per-frame max|y| as its activation scale
+        ya = self.amax_slot(B) if self.precision in F16_PRECS else None
+        ops.upconv3x3(z, out, align_corners, self._aux[key], self._aux[key + "b"], slope, act, y_planes=planes,
+                      y_amax=ya)
+        out._prpe_amax = ya
         if planes:
             out._prpe_planes = True
         return out
@@ -630,7 +644,7 @@ class Engine:
             lin.tile = tile
             self._packs["ir50.output"] = lin
         B = x.shape[0]
-        y = self.conv(x, lin)                                # [B,1,1,512]
+        y = self.conv(x, lin, prec=0, track=False)           # [B,1,1,512]
         emb = self.empty(B, 512)
         norm = self.empty(B, 1)
         ops.l2norm(y.view(B, 512), emb, norm)

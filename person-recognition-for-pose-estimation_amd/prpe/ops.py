@@ -61,13 +61,13 @@ def conv2d(x, pack, y, *, res=None, res_mode=RES_NONE, act=None, precision=0, ti
            scale2=None, bias2=None, act2="none"):
     """y = EPI(conv(PRO(x))) with a ``ConvPack`` (see prpe.pack).
 
-    precision 3 (split fp16) needs ``x_amax``: a [N] device tensor, x_amax[n] bounding max|x[n]|
-    per frame (e.g. the ``y_amax`` its producer raised). ``y_amax`` (any precision): [N] device
-    tensor the kernel raises to max|y[n]| per frame (zero it first)."""
+    precision 3 (split fp16) and 4 (one fp16 plane) need ``x_amax``: a [N] device tensor,
+    x_amax[n] bounding max|x[n]| per frame (e.g. the ``y_amax`` its producer raised). ``y_amax``
+    (any precision): [N] device tensor the kernel raises to max|y[n]| per frame (zero it first)."""
     d = ConvDesc()
     _gpu(pack.w_hi)
     _check_slots(f"prpe_conv2d[{pack.name}]", x.shape[0], x_amax, y_amax, x2_amax)
-    if precision == 3:
+    if precision in (3, 4):
         h16, l16, s16 = pack.f16_planes()
         d.w_h16, d.w_l16, d.scale16 = h16.data_ptr(), l16.data_ptr(), s16.data_ptr()
         d.x_amax = _ptr(x_amax)
@@ -163,15 +163,18 @@ def stem_maxpool(buf, h, w, x_amax, pack, y, y_amax=None):
 
 
 def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none", separable=False,
-              y_planes=False):
-    """Fused one-pass kernel by default; ``separable=True`` runs the two-pass workspace form."""
+              y_planes=False, y_amax=None):
+    """Fused one-pass kernel by default; ``separable=True`` runs the two-pass workspace form.
+    ``y_amax`` ([N] device, zeroed): raised to max|y[n]| per frame (one-pass kernels only)."""
+    _check_slots("prpe_upconv3x3", y.shape[0], y_amax)
     zv, yv = view(z), view(y)
     ws, nbytes = None, 0
     if separable:
         nbytes = lib().prpe_upconv3x3_workspace_bytes(C.byref(zv), C.byref(yv))
         ws = torch.empty((nbytes + 3) // 4, device=z.device, dtype=torch.float32)
     check(lib().prpe_upconv3x3(C.byref(zv), C.byref(yv), 1 if align_corners else 0, _ptr(scale), _ptr(bias),
-                               _ptr(slope), ACT[act], int(y_planes), _ptr(ws), nbytes, _stream()), "prpe_upconv3x3")
+                               _ptr(slope), ACT[act], int(y_planes), _ptr(y_amax), _ptr(ws), nbytes, _stream()),
+          "prpe_upconv3x3")
     return y
 
 

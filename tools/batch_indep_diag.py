@@ -35,8 +35,8 @@ def main():
         rec.append((p.name, y[sel[0]].detach().float().cpu().clone()))
         return y
 
-    def bneck(self, q, x):
-        y = bn0(self, q, x)
+    def bneck(self, q, x, **kw):
+        y = bn0(self, q, x, **kw)
         rec.append((q + ":x_amax", x._prpe_amax[sel[0]:sel[0] + 1].detach().cpu().clone()))
         rec.append((q, y[sel[0]].detach().cpu().clone()))
         rec.append((q + ":y_amax", y._prpe_amax[sel[0]:sel[0] + 1].detach().cpu().clone()))
