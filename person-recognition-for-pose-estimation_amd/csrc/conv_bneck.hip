@@ -399,6 +399,10 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void b
       bl_lds16(q ? wr[2][1] : wr[2][0], w3b + ks * W3_STEP + (q * R3 + rb * 16) * 64, vo, ks * BK_ * 2);
     }
   };
+  // (fence: the x loads above and the W3 pieces stay in separate scheduling regions, so no
+  // counted wait's window can depend on their relative order; tools/barrier_hoist_check.py)
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
   issue_w3(0);
   __syncthreads();
   m2 = wmax2[0];
