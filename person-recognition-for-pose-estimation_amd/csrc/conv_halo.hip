@@ -85,7 +85,11 @@ __device__ __forceinline__ void stage_planes(const float* w, int rows, int cols,
 // WN: waves along N (WN = 2: a 2 x 2 wave grid, wave tile 64 px x BN/2; the B fragments of a
 // K-step are read by 2 waves instead of 4: -20 % LDS reads per MFMA at 4 waves).
 // ONE (precision 4, with F16): one scaled fp16 plane per operand (RNE), one MFMA per product;
-// the B ring stages the weights' hi plane only.
+// the B ring stages the weights' hi plane only. At a third of the MFMAs per tap the fp32 A reads
+// (two ds_read_b128 + the conversion per fragment, every tap) made the kernel LDS-bound, so the
+// chunk's halo is converted ONCE, at its first tap, into an fp16 copy (64 B per pixel, 16-B slot
+// g of pixel q at g ^ ((q >> 2) & 3): 16 consecutive pixels of one slot hit 16 distinct bank
+// groups), and every tap reads one ds_read_b128 per fragment from it. One extra barrier per chunk.
 template <int NW, int TR, int TC, int TN, bool F16, bool APL, int TAPS = 0, int WN = 1, bool ONE = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) void conv_halo_kernel(ConvK p, int tiles_w, int tiles_h) {
   static_assert(TC % 16 == 0 && (TR * TC / 16) % (NW / WN) == 0 && TN % WN == 0, "tile");
@@ -105,7 +109,8 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   static_assert(NB_TOT % NW == 0, "B pieces per wave");
   constexpr int CS = BN / WN + 4;
   constexpr int EPI = NW * 16 * CS * 4;
-  constexpr int MAIN = 2 * HALO + 2 * B_STAGE;
+  constexpr int H16 = ONE ? HQ * 8 * 64 : 0;            // fp16 copy of the current chunk's halo
+  constexpr int MAIN = 2 * HALO + 2 * B_STAGE + H16;
   // w2 (and w3) bf16 planes after the slabs
   constexpr int W2R = TAPS == 2 ? 64 : 32;
   constexpr int W2B = TAPS ? 2 * W2R * (BN + 8) * 2 + (TAPS == 2 ? 2 * 32 * 72 * 2 : 0) : 0;
@@ -113,6 +118,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
   unsigned char* const halo0 = lds;
   unsigned char* const ring = lds + 2 * HALO;
+  unsigned char* const h16 = lds + 2 * HALO + 2 * B_STAGE;
 
   // the wave index through readfirstlane: provably wave-uniform, so the buffer descriptors and
   // LDS-DMA destinations derived from it stay in SGPRs (no waterfall loops around the loads)
@@ -202,7 +208,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
     for (int t = 0; t < 9; ++t) {
       const int px = hb0 + (t / 3) * HW_ + t % 3;
       const int sw = swz_halo(px % HW_);
-      aoff[i][t] = px * 128 + (((2 * fg) ^ sw) << 4);
+      aoff[i][t] = ONE ? px * 64 + ((fg ^ ((px >> 2) & 3)) << 4) : px * 128 + (((2 * fg) ^ sw) << 4);
     }
   }
 
@@ -235,10 +241,30 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         for (int k = t; k < KQ; k += 9)
           if (wave + k * NW < HQ) issue_halo(k, c + 1, (c + 1) & 1);
       }
+      if constexpr (ONE) {
+        if (t == 0) {
+          // the chunk's halo (landed: the barrier above) -> scaled fp16, RNE, once for all taps;
+          // the fp16 copy of the previous chunk is free (every wave is past its last tap)
+          for (int e = tid; e < HP * 4; e += NW * 64) {
+            const int q = e >> 2, g = e & 3;
+            const int sw = swz_halo(q % HW_);
+            const f4 v0 = *reinterpret_cast<const f4*>(hb + q * 128 + (((2 * g) ^ sw) << 4));
+            const f4 v1 = *reinterpret_cast<const f4*>(hb + q * 128 + (((2 * g + 1) ^ sw) << 4));
+            *reinterpret_cast<f16x8*>(h16 + q * 64 + ((g ^ ((q >> 2) & 3)) << 4)) = cvt_f16_one(v0, v1, sa);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
       // A fragments: 8 channels (two 16-B slots) of the tap-shifted pixel
       frag_t af[NP][TM];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
+        if constexpr (ONE) {
+          af[0][i] = *reinterpret_cast<const f16x8*>(h16 + aoff[i][t]);
+          continue;
+        }
         const f4 v0 = *reinterpret_cast<const f4*>(hb + aoff[i][t]);
         const f4 v1 = *reinterpret_cast<const f4*>(hb + (aoff[i][t] ^ 16));
         if constexpr (APL) {
@@ -518,7 +544,9 @@ int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
     if (tile == 32) return kp.w3 ? launch_halo_taps_t<2, 1, 8>(kp, prec, st) : launch_halo_taps_t<1, 1, 8>(kp, prec, st);
     return tile == 30 || tile == 31 ? launch_halo_taps(kp, prec, st) : PRPE_EINVAL;
   }
-  if (tile == 30) tile = kp.Co <= 64 ? 34 : (halo_wn() == 2 ? 36 : 31);
+  // precision 4 takes the 2 x 2 wave grid for Co > 64 (half the B fragment reads per wave; AdaFace
+  // adapter.7 3.05 -> 2.78 ms in the model at bs = 256, profiles/r04_layer_profile_halo_p4_wn2.txt)
+  if (tile == 30) tile = kp.Co <= 64 ? 34 : (halo_wn() == 2 || prec == 4 ? 36 : 31);
   switch (tile) {
     case 31: return launch_halo_kind<4, 8, 16, 8>(kp, prec, st);     // 8 x 16 px, 4 waves, 128 ch
     case 32: return launch_halo_kind<8, 16, 16, 8>(kp, prec, st);    // 16 x 16 px, 8 waves, 128 ch

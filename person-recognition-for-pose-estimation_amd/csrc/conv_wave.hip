@@ -52,7 +52,10 @@ constexpr int BK = 32;
 // ONE (precision 4, with F16): ONE scaled fp16 plane per operand (RNE), one MFMA per product
 // instead of three; the weights' hi plane alone (w_h16 = RNE(w 2^e[co])) is staged. Allows the
 // prologue affine: the activation scale then comes from a bound of the prologue's output
-// (prologue_bounds, conv.h).
+// (prologue_bounds, conv.h). With a third of the MFMAs per K-step the per-step barrier would
+// dominate, so one iteration covers TWO K-steps (KS = 2): the B stage holds the hi plane of
+// K-steps 2s and 2s+1 where the two-plane forms hold two planes of one step (same 16 KB at
+// BN = 128), and each accumulator takes step 2s then 2s+1 (the sequential order).
 template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false,
           bool APL = false, bool ONE = false>
 __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
@@ -61,10 +64,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   static_assert(!ONE || (F16 && !DUAL && !APL), "single fp16 plane: precision 4");
   static_assert(!DUAL || !PRO, "dual input: no prologue");
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
-  constexpr int NPL = ONE ? 1 : NP;                   // planes staged and multiplied
+  // K-steps per iteration: 2 for ONE, except the 8-wave prologue tile (154 VGPRs at 2 steps: one
+  // workgroup per CU instead of two, 56x56 IR-50 res_layer convs +12 %)
+  constexpr int KS = ONE && !(PRO && NW == 8) ? 2 : 1;
+  constexpr int NSL = ONE ? KS : NP;                  // B stage slices: planes, or (ONE) K-steps
   constexpr int WTM = TM * 16, BM = NW * WTM, BN = TN * 16;
-  constexpr int B_STAGE = NPL * BN * 64;              // bf16 / f16 [NPL][BN][32]
-  constexpr int NB_TOT = NPL * BN / 16;               // 1-KiB LDS-DMA pieces per stage
+  constexpr int B_STAGE = NSL * BN * 64;              // bf16 / f16 [NSL][BN][32]
+  constexpr int NB_TOT = NSL * BN / 16;               // 1-KiB LDS-DMA pieces per stage
   constexpr int IB = (NB_TOT + NW - 1) / NW;          // per wave (surplus slots repeat a piece)
   constexpr int CS = BN + 4;                          // epilogue row pitch (floats)
   constexpr int EPI = NW * 16 * CS * 4;
@@ -147,7 +153,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   // ---- B pieces: piece j -> plane j / (BN/16), rows 16 (j % (BN/16)) .. +16; lane -> (row, slot),
   // through one descriptor per plane (the K-step's 64 B as soffset)
   const int wbytes = p.k_pad * 2 * (p.tiles_n * BN);
-  const uint16_t* planes[3] = {F16 ? p.wh16 : p.whi, F16 ? p.wl16 : p.wlo, p.wlo2};
+  const uint16_t* planes[3] = {F16 ? p.wh16 : p.whi, ONE ? p.wh16 : (F16 ? p.wl16 : p.wlo), p.wlo2};
   unsigned bvo[IB];
   int bdst[IB];
   int bq[IB];
@@ -162,18 +168,19 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     bdst[i] = (q * BN + rb * 16) * 64;
     bq[i] = q;                                          // wave-uniform
   }
-  __amdgpu_buffer_rsrc_t wr[NPL];
+  __amdgpu_buffer_rsrc_t wr[NSL];
 #pragma unroll
-  for (int q = 0; q < NPL; ++q) wr[q] = buf_rsrc(planes[q], wbytes);
+  for (int q = 0; q < NSL; ++q) wr[q] = buf_rsrc(planes[q], wbytes);
+  // kt: the iteration; ONE: slice q of its stage is K-step 2 kt + q of the hi plane
   auto issue_b = [&](int kt, int stage) {
     unsigned char* sb = lds + stage * B_STAGE;
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
       __amdgpu_buffer_rsrc_t r = wr[0];
 #pragma unroll
-      for (int q = 1; q < NPL; ++q)
+      for (int q = 1; q < NSL; ++q)
         if (bq[i] == q) r = wr[q];
-      bl_lds16(r, sb + bdst[i], bvo[i], kt * BK * 2);
+      bl_lds16(r, sb + bdst[i], bvo[i], (ONE ? KS * kt + bq[i] : kt) * BK * 2);
     }
   };
 
@@ -181,17 +188,22 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   int u_kh = 0, u_kw = 0, u_ci = 0, u_step = 0;
   int u_off = 0;                                      // kh*xsh + kw*xsw + chunk*32 (elements)
   const int nk = p.nk;
-  f4 raw[TM][2];
-  unsigned amask = 0;
-  f4 as4[2], ab4[2];
-  auto load_a = [&]() {
+  f4 raw[KS][TM][2];
+  unsigned amask[KS];
+  f4 as4[KS][2], ab4[KS][2];
+  // the A operand of the walk's current K-step into sub-step slot ks, then advance the walk
+  int u_cnt = 0;                                      // K-steps loaded so far (ONE: odd nk pads one)
+  auto load_a = [&](int ks) {
+    // ONE with odd nk: the last iteration's second step is a phantom (k >= K): zero A, so it adds
+    // nothing whatever the B slice holds
+    const bool phantom = ONE && u_cnt++ >= nk;
     if constexpr (PRO) {
-      as4[0] = *reinterpret_cast<const f4*>(p.in_scale + u_ci + fg * 8);
-      as4[1] = *reinterpret_cast<const f4*>(p.in_scale + u_ci + fg * 8 + 4);
-      ab4[0] = *reinterpret_cast<const f4*>(p.in_bias + u_ci + fg * 8);
-      ab4[1] = *reinterpret_cast<const f4*>(p.in_bias + u_ci + fg * 8 + 4);
+      as4[ks][0] = *reinterpret_cast<const f4*>(p.in_scale + u_ci + fg * 8);
+      as4[ks][1] = *reinterpret_cast<const f4*>(p.in_scale + u_ci + fg * 8 + 4);
+      ab4[ks][0] = *reinterpret_cast<const f4*>(p.in_bias + u_ci + fg * 8);
+      ab4[ks][1] = *reinterpret_cast<const f4*>(p.in_bias + u_ci + fg * 8 + 4);
     }
-    amask = 0;
+    amask[ks] = 0;
     const bool second = DUAL && u_step >= p.nk1;     // wave-uniform
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -199,18 +211,18 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
       if constexpr (DUAL) {
         if (second) {                                   // x2: 1x1, never padded
           const int so = (u_off - p.nk1 * BK) * 4;
-          raw[i][0] = bl_f4(x2r, rv2[i], so);
-          raw[i][1] = bl_f4(x2r, rv2[i] + 16, so);
+          raw[ks][i][0] = bl_f4(x2r, rv2[i], so);
+          raw[ks][i][1] = bl_f4(x2r, rv2[i] + 16, so);
         } else {
-          raw[i][0] = bl_f4(xr, rv[i], u_off * 4);
-          raw[i][1] = bl_f4(xr, rv[i] + 16, u_off * 4);
+          raw[ks][i][0] = bl_f4(xr, rv[i], u_off * 4);
+          raw[ks][i][1] = bl_f4(xr, rv[i] + 16, u_off * 4);
         }
       } else {
-        const unsigned v = ok ? rv[i] : BL_OOB;
-        raw[i][0] = bl_f4(xr, v, u_off * 4);
-        raw[i][1] = bl_f4(xr, v + 16, u_off * 4);
+        const unsigned v = ok && !phantom ? rv[i] : BL_OOB;
+        raw[ks][i][0] = bl_f4(xr, v, u_off * 4);
+        raw[ks][i][1] = bl_f4(xr, v + 16, u_off * 4);
       }
-      if constexpr (PRO) amask |= (unsigned)ok << i;
+      if constexpr (PRO) amask[ks] |= (unsigned)(ok && !phantom) << i;
     }
     // advance to the next K-step (kw, then kh, then the next chunk); stay on the last one
     if (++u_step < nk) {
@@ -224,21 +236,23 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     }
   };
 
-  frag_t af[NP][TM];
+  frag_t af[NP][TM];                                  // planes, or (ONE) K sub-steps
   auto split_a = [&]() {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      f4 v0 = raw[i][0], v1 = raw[i][1];
+#pragma unroll
+     for (int ks = 0; ks < KS; ++ks) {
+      f4 v0 = raw[ks][i][0], v1 = raw[ks][i][1];
       if constexpr (PRO) {
-        v0 = v0 * as4[0] + ab4[0];
-        v1 = v1 * as4[1] + ab4[1];
-        if (!((amask >> i) & 1u)) { v0 = f4{0.f, 0.f, 0.f, 0.f}; v1 = v0; }   // padding stays 0
+        v0 = v0 * as4[ks][0] + ab4[ks][0];
+        v1 = v1 * as4[ks][1] + ab4[ks][1];
+        if (!((amask[ks] >> i) & 1u)) { v0 = f4{0.f, 0.f, 0.f, 0.f}; v1 = v0; }   // padding stays 0
       }
       if constexpr (APL) {
         af[0][i] = __builtin_bit_cast(bf16x8, v0);
         af[1][i] = __builtin_bit_cast(bf16x8, v1);
       } else if constexpr (ONE) {
-        af[0][i] = cvt_f16_one(v0, v1, sa[i]);
+        af[ks][i] = cvt_f16_one(v0, v1, sa[i]);
       } else if constexpr (F16) {
         unsigned long long p0[2], p1[2];
         split_planes_f16(v0, sa[i], p0);
@@ -256,6 +270,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
         for (int q = 0; q < NP; ++q)
           af[q][i] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
       }
+     }
     }
   };
 
@@ -271,13 +286,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     for (int j = 0; j < TN; ++j) {
       const int nrow = j * 16 + fr;
       const unsigned char* bp = sb + nrow * 64 + ((fg ^ swzF(nrow)) << 4);
-      frag_t bfr[NP];
+      frag_t bfr[NSL];
 #pragma unroll
-      for (int q = 0; q < NPL; ++q) bfr[q] = *reinterpret_cast<const frag_t*>(bp + q * BN * 64);
+      for (int q = 0; q < NSL; ++q) bfr[q] = *reinterpret_cast<const frag_t*>(bp + q * BN * 64);
       // partial products smallest first; terms with plane-index sum >= NP are dropped
-      if constexpr (ONE) {
+      if constexpr (ONE) {                            // K-step KS kt, then KS kt + 1
 #pragma unroll
-        for (int i = 0; i < TM; ++i) acc[i][j] = mfma16(af[0][i], bfr[0], acc[i][j]);
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) acc[i][j] = mfma16(af[ks][i], bfr[ks], acc[i][j]);
         continue;
       }
 #pragma unroll
@@ -290,10 +307,15 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
     }
   };
 
-  // ---------------- main loop
-  load_a();
+  // ---------------- main loop (nit iterations of KS K-steps)
+  const int nit = (nk + KS - 1) / KS;
+  auto load_it = [&]() {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) load_a(ks);
+  };
+  load_it();
   issue_b(0, 0);
-  if constexpr (STAGES == 3) issue_b(nk > 1 ? 1 : 0, 1);
+  if constexpr (STAGES == 3) issue_b(nit > 1 ? 1 : 0, 1);
   split_a();
   // planes input: the A fragments of step 0 ARE the load destinations (no split), so the
   // compiler's wait bookkeeping would carry their pending loads into the loop header and merge
@@ -303,12 +325,12 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   // its overlap (STAGES 2 waits for them at the loop top anyway).
   if constexpr (APL) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
   int st = 0;
-  for (int kt = 0; kt < nk; ++kt) {
+  for (int kt = 0; kt < nit; ++kt) {
     // B(kt) of this wave: at most the (STAGES-2)*IB pieces issued after it are still pending
     wait_barrier<(STAGES - 2) * IB>();
-    load_a();
+    load_it();
     {
-      const int ks = kt + STAGES - 1 < nk ? kt + STAGES - 1 : nk - 1;
+      const int ks = kt + STAGES - 1 < nit ? kt + STAGES - 1 : nit - 1;
       const int sn = st == 0 ? STAGES - 1 : st - 1;   // the stage read at kt-1
       issue_b(ks, sn);
     }
@@ -557,8 +579,8 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
     }
   }
   if (prec == 4) {                                     // the precision-3 shapes, one fp16 plane
+    // (no 256 x 128 / 64 x 128-wave tile: at two K-steps per iteration it spills)
     switch (tile) {
-      case 24: return launch<4, 4, 8, 2, 3, true, true>(kp, st);
       case 25: return launch<8, 2, 4, 2, 3, true, true>(kp, st);   // 256 x 64, wave 32 x 64
       case 26: return launch<4, 2, 8, 2, 3, true, true>(kp, st);   // 128 x 128, 3 stages
       case 27: return launch<4, 2, 8, 2, 2, true, true>(kp, st);   // 128 x 128, 2 stages

@@ -101,7 +101,7 @@ P4_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("tile", [0, 24, 25, 26, 27])
+@pytest.mark.parametrize("tile", [0, 25, 26, 27])
 @pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", P4_SHAPES)
 def test_conv_p4_matches_operand_emulation(B, Ci, H, W, Co, k, s, p, tile):
     x = torch.relu(rnd(B, Ci, H, W, seed=401)) * 7.0
