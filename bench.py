@@ -72,7 +72,8 @@ CONFIGS = {
                 "ViTPose-B keypoint head on 256x192 crops (pixel_values -> heatmaps -> soft-argmax)"),
 }
 DTYPE = ("f32 storage/accumulate; split-operand MFMA: trunk 2x fp16 planes (3 terms), YOLO net 3x bf16 "
-         "(6 terms), adapters/IR-50/ViT 2x bf16 (3 terms)")
+         "(6 terms), YOLO / ViT adapters and ViT 2x bf16 (3 terms), AdaFace adapter 3x3s + IR-50 1x fp16 "
+         "plane with per-frame power-of-2 scaling (1 term)")
 
 
 def parse():
@@ -302,7 +303,8 @@ def main():
                      and t.get("layer") in dominant and t.get("precision") == precn)
             if fresh:
                 roof["traffic"] = round(t["hbm_bytes_per_launch"] / 1e9, 3)
-                roof["traffic_unit"] = "GB per launch (PMC FETCH_SIZE x2 + WRITE_SIZE)"
+                roof["traffic_unit"] = ("GB per launch, L2-to-fabric bytes incl. Infinity-Cache hits "
+                                        "(PMC FETCH_SIZE x2 + WRITE_SIZE)")
                 roof["algorithmic_gb_per_launch"] = round(t["algorithmic_bytes_per_launch"] / 1e9, 3)
                 roof["traffic_source"] = os.path.relpath(tp, ROOT)
             else:
