@@ -544,12 +544,18 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       const char* e = getenv("PRPE_WAVE_WIDE3");
       return e ? atoi(e) : 27;
     }();
+    // PRPE_WAVE_P4=<26|27> overrides the precision-4 choice for Co > 64 (A/B runs)
+    static const int wide4 = [] {
+      const char* e = getenv("PRPE_WAVE_P4");
+      return e && atoi(e) == 26 ? 26 : 27;
+    }();
     static const int tile2 = [] {
       const char* e = getenv("PRPE_WAVE_P2");
       return e ? atoi(e) : 27;
     }();
     if (prec == 0) tile = wide;
-    else if (prec >= 3) tile = kp.Co > 64 && (kp.K > 128 || p3_smallk_wide) ? wide3 : p3_narrow;
+    else if (prec == 3) tile = kp.Co > 64 && (kp.K > 128 || p3_smallk_wide) ? wide3 : p3_narrow;
+    else if (prec == 4) tile = kp.Co > 64 ? wide4 : 25;  // (the precision-3 overrides do not apply)
     else tile = kp.Co > 64 && kp.K > 128 ? tile2 : 24;
   }
   if (prec == 0) {
