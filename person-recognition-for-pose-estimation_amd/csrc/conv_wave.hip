@@ -540,9 +540,13 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       const char* e = getenv("PRPE_WAVE_P3_SMALLK");
       return e && e[0] == '0' ? 0 : 1;
     }();
+    // precision 3, Co > 64: the 256 x 128 8-wave tile (wave 32 x 128, 3-stage ring) since round 4:
+    // trunk convs 68.6 -> 66.1 ms at bs = 256 against the 128 x 128 2-stage tile, every unfused
+    // trunk conv faster (profiles/r04_layer_profile_trunk_wide3_sweep.txt; round 2 had measured the
+    // opposite, before the buffer-descriptor addressing of round 3)
     static const int wide3 = [] {
       const char* e = getenv("PRPE_WAVE_WIDE3");
-      return e ? atoi(e) : 27;
+      return e ? atoi(e) : 23;
     }();
     // PRPE_WAVE_P4=<26|27> overrides the precision-4 choice for Co > 64 (A/B runs)
     static const int wide4 = [] {
