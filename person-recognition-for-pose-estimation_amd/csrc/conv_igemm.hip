@@ -760,9 +760,15 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const char* e = getenv("PRPE_CONV_GEMM_P3");
     return e && e[0] == '1' ? 1 : 0;
   }();
+  // PRPE_GEMM_TILE=41|42 overrides the automatic GEMM tile (A/B runs)
+  static const int gemm_tile = [] {
+    const char* e = getenv("PRPE_GEMM_TILE");
+    const int t = e ? atoi(e) : 40;
+    return t == 41 || t == 42 ? t : 40;
+  }();
   if (tile == 0 && gemm_on && (kp.x_planes || (prec == 3 && gemm_p3)) && kp.M >= (1 << 15) &&
       conv_gemm_eligible(kp, prec))
-    return conv_gemm_launch(kp, prec, 40, st);
+    return conv_gemm_launch(kp, prec, gemm_tile, st);
   if (tile >= 30 && tile < 40)
     return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;
   if (tile == 0 && halo_on && conv_halo_auto(kp, prec) && conv_halo_eligible(kp, prec, km))
