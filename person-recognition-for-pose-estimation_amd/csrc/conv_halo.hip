@@ -540,6 +540,14 @@ bool conv_halo_auto(const ConvK& kp, int prec) {
 // per workgroup, or 64 when Co <= 64 (tools/conv_bench.py, profiles/r02_conv_bench_halo.txt);
 // 31..35 force a configuration
 int conv_halo_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
+  // PRPE_HALO_TILE=32 / 33 makes that tile the automatic choice for Co > 64 (A/B runs; for the
+  // epilogue-GEMM convs 32 selects the 16 x 16-pixel 8-wave form)
+  static const int env_tile = [] {
+    const char* e = getenv("PRPE_HALO_TILE");
+    const int t = e ? atoi(e) : 0;
+    return t == 32 || t == 33 ? t : 0;
+  }();
+  if (tile == 30 && env_tile && kp.Co > 64 && (!kp.w2 || env_tile == 32)) tile = env_tile;
   if (kp.w2) {
     if (tile == 32) return kp.w3 ? launch_halo_taps_t<2, 1, 8>(kp, prec, st) : launch_halo_taps_t<1, 1, 8>(kp, prec, st);
     return tile == 30 || tile == 31 ? launch_halo_taps(kp, prec, st) : PRPE_EINVAL;

@@ -715,7 +715,7 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     return conv_splitk_launch(kp, static_cast<float*>(d->workspace), st);
   }
   // epilogue 1x1 GEMM: the haloed-tile kernel's 128-column tile is the only implementation
-  if (kp.w2) return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile ? tile : 31, st) : PRPE_EINVAL;
+  if (kp.w2) return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile ? tile : 30, st) : PRPE_EINVAL;
   if (tile == 0 && y.c <= 4 && km == 1 && !d->in_scale && d->w_lo && d->w_lo2 && x.c <= 256 && khw == 1) {
     int lg = 0;
     while ((1 << lg) * 4 < x.c) ++lg;

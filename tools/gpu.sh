@@ -12,6 +12,7 @@
 #   bash tools/gpu.sh traffic TAG KERNEL MIN_US ALG_BYTES LAYER BATCH PREC SOURCES SHAPE -- python-args...
 #                                                FETCH_SIZE / WRITE_SIZE passes -> gpurun_out/TAG_traffic.json
 #   bash tools/gpu.sh py TAG SECONDS -- python-args...   any tool script -> gpurun_out/TAG.txt
+#   bash tools/gpu.sh evidence rNN               traffic records of the four configs, kernel trace, bench lines
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 9
 O=gpurun_out
@@ -60,6 +61,32 @@ case "$cmd" in
       --batch "$BATCH" --precision "$PREC" --algorithmic "$ALG" --sources "$SRCS" --shape "$SHAPE" \
       --out $O/${TAG}_traffic.json --command "tools/gpu.sh traffic $TAG"
     rc=$?; rm -rf $O/${TAG}_FETCH_SIZE $O/${TAG}_WRITE_SIZE; cat $O/${TAG}_traffic.json; exit $rc ;;
+  evidence)
+    # end-of-round record on the committed sources: PMC traffic of every bench config's dominant
+    # launch (profiles/rNN_pmc_traffic_<config>.json, read by bench.py while the sources match),
+    # the kernel trace of the bench command, and the four bench lines with CPU baselines
+    R=$1; [ -n "$R" ] || { echo "evidence needs the round tag (e.g. r04)"; exit 9; }
+    bash tools/gpu.sh traffic ${R}_full conv_halo 5000 14245036032 vit_pose.adapter.7 256 0 conv_halo.hip,conv.h,common.h \
+      "3x3 256->128 @256x192, planes input, GELU, epilogue tap GEMM to 27 ch" -- tools/conv_bench.py --only vit_adapter.7 \
+      --prec 0 --tiles 0 --korders 1 --batch 256 --iters 2 --planes --act gelu --taps 27 || exit 11
+    bash tools/gpu.sh traffic ${R}_yolo_face "conv_halo_kernel<4, 8, 16, 8, false, true, 2" 1000 1855848448 yolo_face.adapter.10 64 0 \
+      conv_halo.hip,conv.h,common.h "3x3 256->128 @160x160, planes input, SiLU, epilogue chain 1x1 128->64 + SiLU -> 27 taps" \
+      -- bench.py --config yolo_face --steps 2 --warmup 1 --no-cpu-baseline || exit 12
+    bash tools/gpu.sh traffic ${R}_vitpose conv_gemm_kernel 300 764411904 "vit_pose.vit_pose.backbone.encoder.layer.0:fc1" 256 0 \
+      conv_gemm.hip,conv.h,common.h "1x1 768->3072 over 49152 tokens, planes input and output, GELU" \
+      -- tools/conv_bench.py --only "vit fc1" --prec 0 --tiles 0 --korders 0 --batch 256 --iters 3 --planes --act gelu || exit 13
+    # yolo_raw: p1.0 (3x3/2 3->16 on the raw NCHW frames; algorithmic = 64 frames in + the 16-ch map out)
+    bash tools/gpu.sh traffic ${R}_yolo_raw "conv_igemm_kernel<128, 16" 300 734004928 yolo_face.yolo.net.p1.0 64 2 \
+      conv_igemm.hip,conv.h,common.h "3x3/2 3->16 @640x640, NCHW frames read in place" \
+      -- bench.py --config yolo_raw --steps 2 --warmup 1 --no-cpu-baseline || exit 14
+    for C in full yolo_face vitpose yolo_raw; do
+      mv $O/${R}_${C}_traffic.json $O/${R}_pmc_traffic_${C}.json && cp $O/${R}_pmc_traffic_${C}.json profiles/ || exit 15
+    done
+    bash tools/gpu.sh trace ${R}_final || exit 16
+    for C in full yolo_face vitpose yolo_raw; do
+      timeout -k 10 400 python bench.py --config $C --steps 20 --warmup 3 > $O/${R}_bench_${C}.json 2> $O/${R}_bench_${C}.err || exit 17
+      tail -c 300 $O/${R}_bench_${C}.json
+    done ;;
   py)
     TAG=$1 SEC=$2; shift 2; [ "$1" = "--" ] && shift
     timeout -k 10 "$SEC" python3 -u "$@" > $O/${TAG}.txt 2>&1
