@@ -266,6 +266,7 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
   __shared__ __attribute__((aligned(1024))) float ring[UPD_RING][UPD_NI * 256];
   __shared__ int ty0[UP_MAX_R + 2];
   __shared__ float tly[UP_MAX_R + 2];
+  __shared__ int thi[UP_MAX_R];                        // hi_at(oy) per output row (below)
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   int t = bid;
   const int cb = t % cblocks;
@@ -372,6 +373,10 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
     }
     return h;
   };
+  // ... tabulated once per block (one LDS read per output row in the loop instead of three and
+  // the selects; the row loop is VALU-bound: ~160 VALU per thread and row, profiles/r04_pmc_upconv.txt)
+  for (int e = threadIdx.x; e < oy1 - oy0; e += 256) thi[e] = hi_at(oy0 + e);
+  __syncthreads();
   int lo_row = Hi;
 #pragma unroll
   for (int dy = 0; dy < 3; ++dy) {
@@ -386,11 +391,16 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
 
   const int yo = ox * (int)p.y.sw + (c0 + cg * 4) * (int)p.y.sc;
   float* yn = p.y.ptr + (int64_t)n * p.y.sn;
-  float hA[3][4], hB[3][4];
+  // x-interpolated rows y0 (A) and y0 + 1 (B) of each dy in two register slots whose roles a
+  // wave-uniform parity bit says (par 0: A = h0, B = h1): moving down one source row flips the
+  // parity and refills the old A slot, so no register copies (the hA = hB rolling form made the
+  // compiler move 8 registers per dy and row on every path)
+  float h0[3][4], h1[3][4];
   int cur[3] = {-2, -2, -2};
+  int par[3] = {0, 0, 0};
   float ym = 0.f;
   for (int oy = oy0; oy < oy1; ++oy) {
-    const int need = __builtin_amdgcn_readfirstlane(hi_at(oy));
+    const int need = __builtin_amdgcn_readfirstlane(thi[oy - oy0]);
     if (need > in_use) {
       // the row(s) coming into use were DMA'd at the previous such event, >= UPD_MIN output rows
       // (stores) ago: wait for everything older than those stores, then publish every wave's
@@ -411,16 +421,23 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
       const int y1 = y0 < Hi - 1 ? y0 + 1 : y0;
       if (y0 != cur[dy]) {
         if (y0 == cur[dy] + 1) {
-#pragma unroll
-          for (int v = 0; v < 4; ++v) hA[dy][v] = hB[dy][v];
+          par[dy] ^= 1;                                // old B (row y0) is the new A
+        } else if (par[dy]) {
+          hrow(y0, dy, h1[dy]);
         } else {
-          hrow(y0, dy, hA[dy]);
+          hrow(y0, dy, h0[dy]);
         }
-        hrow(y1, dy, hB[dy]);
+        if (par[dy]) hrow(y1, dy, h0[dy]);             // B: the slot A does not use
+        else hrow(y1, dy, h1[dy]);
         cur[dy] = y0;
       }
+      if (par[dy]) {
 #pragma unroll
-      for (int v = 0; v < 4; ++v) acc[v] = lerp_add(acc[v], ly, hA[dy][v], hB[dy][v]);
+        for (int v = 0; v < 4; ++v) acc[v] = lerp_add(acc[v], ly, h1[dy][v], h0[dy][v]);
+      } else {
+#pragma unroll
+        for (int v = 0; v < 4; ++v) acc[v] = lerp_add(acc[v], ly, h0[dy][v], h1[dy][v]);
+      }
     }
     if (!live) continue;
     f32x4 pre;
