@@ -120,6 +120,12 @@ __device__ __forceinline__ f16x8 cvt_f16_one(f4 v0, f4 v1, float sa) {
   return f16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
 }
 
+// the input-side affine s x + b, fused (one rounding per element), so the wave-row and
+// haloed-tile kernels round the prologue's output identically
+__device__ __forceinline__ f4 affine4(f4 v, f4 s, f4 b) {
+  return f4{fmaf(v[0], s[0], b[0]), fmaf(v[1], s[1], b[1]), fmaf(v[2], s[2], b[2]), fmaf(v[3], s[3], b[3])};
+}
+
 // precision 4 with an input-side affine (IR-50 pre-BN prologue): an upper bound of
 // max|s x + b| over the frame = amax(x) max|s| + max|b|, with max|s| and max|b| over the Ci
 // prologue channels reduced here (every lane gets the wave's maxima). A loose bound only costs

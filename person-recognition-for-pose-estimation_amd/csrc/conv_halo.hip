@@ -186,10 +186,18 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       bl_lds16(bpl[i] ? wr1 : wr0, sb + bdst[i], bvo[i], kt * HBK * 2);
   };
 
-  // precision 3: one frame per block -> one activation scale
+  // precision 3: one frame per block -> one activation scale. Precision 4 may carry the
+  // input-side affine (pro): the scale then comes from the bound of its output, as in conv_wave.hip
+  const bool pro = ONE && p.in_scale != nullptr;       // kernel-uniform
   float sa = 1.f, inv = 1.f;
   if constexpr (F16) {
-    const int e = f16_scale_exp(p.x_amax[n]);
+    float am = p.x_amax[n];
+    if (pro) {
+      float pS, pB;
+      prologue_bounds(p.in_scale, p.in_bias, p.Ci, pS, pB);
+      am = fmaf(am, pS, pB);
+    }
+    const int e = f16_scale_exp(am);
     sa = ldexpf(1.f, 15 - e);
     inv = ldexpf(1.f, e - 15);
   }
@@ -244,12 +252,29 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       if constexpr (ONE) {
         if (t == 0) {
           // the chunk's halo (landed: the barrier above) -> scaled fp16, RNE, once for all taps;
-          // the fp16 copy of the previous chunk is free (every wave is past its last tap)
+          // the fp16 copy of the previous chunk is free (every wave is past its last tap).
+          // pro: s x + b first on the pixels inside the frame, the padding stays 0 (the reference
+          // pads the affine's output). A thread's slot g = tid & 3 is the same at every e.
+          f4 ps4[2], pb4[2];
+          if (pro) {
+            const int ch = c * HBK + (tid & 3) * 8;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              ps4[h] = *reinterpret_cast<const f4*>(p.in_scale + ch + 4 * h);
+              pb4[h] = *reinterpret_cast<const f4*>(p.in_bias + ch + 4 * h);
+            }
+          }
           for (int e = tid; e < HP * 4; e += NW * 64) {
             const int q = e >> 2, g = e & 3;
-            const int sw = swz_halo(q % HW_);
-            const f4 v0 = *reinterpret_cast<const f4*>(hb + q * 128 + (((2 * g) ^ sw) << 4));
-            const f4 v1 = *reinterpret_cast<const f4*>(hb + q * 128 + (((2 * g + 1) ^ sw) << 4));
+            const int hr = q / HW_, hc = q - hr * HW_;
+            const int sw = swz_halo(hc);
+            f4 v0 = *reinterpret_cast<const f4*>(hb + q * 128 + (((2 * g) ^ sw) << 4));
+            f4 v1 = *reinterpret_cast<const f4*>(hb + q * 128 + (((2 * g + 1) ^ sw) << 4));
+            if (pro) {
+              const bool in = (unsigned)(oh0 - 1 + hr) < (unsigned)p.Hi && (unsigned)(ow0 - 1 + hc) < (unsigned)p.Wi;
+              v0 = in ? affine4(v0, ps4[0], pb4[0]) : f4{0.f, 0.f, 0.f, 0.f};
+              v1 = in ? affine4(v1, ps4[1], pb4[1]) : f4{0.f, 0.f, 0.f, 0.f};
+            }
             *reinterpret_cast<f16x8*>(h16 + q * 64 + ((g ^ ((q >> 2) & 3)) << 4)) = cvt_f16_one(v0, v1, sa);
           }
           __builtin_amdgcn_sched_barrier(0);
@@ -514,12 +539,12 @@ bool conv_halo_eligible(const ConvK& kp, int prec, int km) {
   // 3x3 / stride 1 / pad 1 over whole 32-channel chunks (chunk-major weights), vectorised
   // epilogue, precision 0 (fp32 or planes input) or 3 (fp16 planes + the input's max bound)
   const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.x_planes;
-  const bool p4 = prec == 4 && kp.wh16 && kp.x_amax && !kp.x_planes;
+  const bool p4 = prec == 4 && kp.wh16 && kp.x_amax && !kp.x_planes && (!kp.in_scale || kp.in_bias);
   // buffer descriptors: one frame of x and one weight plane each < 2^31 bytes (32-bit offsets)
   const int64_t frame_bytes = ((int64_t)(kp.Hi - 1) * kp.xsh + (int64_t)(kp.Wi - 1) * kp.xsw + kp.Ci) * 4;
   const int64_t w_bytes = (int64_t)kp.k_pad * 2 * (((kp.Co + 127) / 128) * 128);
   return km == 2 && kp.KH == 3 && kp.KW == 3 && kp.stride == 1 && kp.pad == 1 && kp.Ci % HBK == 0 &&
-         kp.vec_out && (prec == 0 || p3 || p4) && !kp.in_scale && !kp.x2 && kp.k_pad == kp.K && kp.zero &&
+         kp.vec_out && (prec == 0 || p3 || p4) && (!kp.in_scale || p4) && !kp.x2 && kp.k_pad == kp.K && kp.zero &&
          kp.Hi == kp.Ho && kp.Wi == kp.Wo && kp.xsh >= 0 && kp.xsw >= 0 && frame_bytes < (1LL << 31) &&
          w_bytes < (1LL << 31);
 }
@@ -529,7 +554,12 @@ bool conv_halo_eligible(const ConvK& kp, int prec, int km) {
 // slower on 8 x 16 tiles), and an fp32-input precision-0 conv stays on the wave kernel (the
 // AdaFace adapter's 128->64 ran 8 % slower); planes input and precision 3 win (adapters' 3x3
 // 256->128 -3..-5 %, trunk layer1 3x3 -10 %).
+// Precision 4 (one MFMA per product, so the wave kernel's per-tap A loads weigh three times as
+// much) takes it from 14 x 14 up whatever the waste: the IR-50 body's 14x14 256->256 -38 %,
+// 28x28 128->128 -21 %, 56x56 64->64 -30 % at bs = 256 (profiles/r04_conv_bench_ir50_halo.txt);
+// 7 x 7 stays on the wave kernel (one 8 x 16 tile per frame, 2.6x waste: no gain).
 bool conv_halo_auto(const ConvK& kp, int prec) {
+  if (prec == 4 && kp.Ho >= 14 && kp.Wo >= 14) return true;
   if (prec == 0 && !kp.x_planes) return false;
   const int tc = 16, tr = 8;
   const int64_t covered = (int64_t)((kp.Ho + tr - 1) / tr) * tr * ((kp.Wo + tc - 1) / tc) * tc;

@@ -57,7 +57,7 @@ constexpr int BK = 32;
 // K-steps 2s and 2s+1 where the two-plane forms hold two planes of one step (same 16 KB at
 // BN = 128), and each accumulator takes step 2s then 2s+1 (the sequential order).
 template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false,
-          bool APL = false, bool ONE = false>
+          bool APL = false, bool ONE = false, int KSF = 0>
 __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   static_assert(!APL || (NP == 2 && !F16 && !PRO && !DUAL), "planes input: two bf16 planes only");
   static_assert(!F16 || (NP == 2 && (!PRO || ONE)), "f16 planes: two planes, no prologue unless single-plane");
@@ -66,7 +66,8 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
   // K-steps per iteration: 2 for ONE, except the 8-wave prologue tile (154 VGPRs at 2 steps: one
   // workgroup per CU instead of two, 56x56 IR-50 res_layer convs +12 %)
-  constexpr int KS = ONE && !(PRO && NW == 8) ? 2 : 1;
+  // (KSF = 1 forces one K-step: 128 instead of 160 VGPRs on the 128 x 128 tile, 4 workgroups per CU)
+  constexpr int KS = ONE && !(PRO && NW == 8) && KSF != 1 ? 2 : 1;
   constexpr int NSL = ONE ? KS : NP;                  // B stage slices: planes, or (ONE) K-steps
   constexpr int WTM = TM * 16, BM = NW * WTM, BN = TN * 16;
   constexpr int B_STAGE = NSL * BN * 64;              // bf16 / f16 [NSL][BN][32]
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   // PRO (precision 4 only): max|in_scale x + in_bias| <= max|x| pS + pB
   float pS = 1.f, pB = 0.f;
   if constexpr (F16 && PRO) prologue_bounds(p.in_scale, p.in_bias, p.Ci, pS, pB);
-  auto bound = [&](float am) { return PRO ? am * pS + pB : am; };
+  auto bound = [&](float am) { return PRO ? fmaf(am, pS, pB) : am; };
   if constexpr (F16) {
     if (two) {
       if (wrow0 < p.M) am0 = bound(DUAL ? fmaxf(p.x_amax[nf0], p.x2_amax[nf0]) : p.x_amax[nf0]);
@@ -244,8 +245,13 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
      for (int ks = 0; ks < KS; ++ks) {
       f4 v0 = raw[ks][i][0], v1 = raw[ks][i][1];
       if constexpr (PRO) {
-        v0 = v0 * as4[ks][0] + ab4[ks][0];
-        v1 = v1 * as4[ks][1] + ab4[ks][1];
+        if constexpr (ONE) {                          // (as conv_halo.hip's precision-4 prologue)
+          v0 = affine4(v0, as4[ks][0], ab4[ks][0]);
+          v1 = affine4(v1, as4[ks][1], ab4[ks][1]);
+        } else {
+          v0 = v0 * as4[ks][0] + ab4[ks][0];
+          v1 = v1 * as4[ks][1] + ab4[ks][1];
+        }
         if (!((amask[ks] >> i) & 1u)) { v0 = f4{0.f, 0.f, 0.f, 0.f}; v1 = v0; }   // padding stays 0
       }
       if constexpr (APL) {
@@ -450,7 +456,7 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
   }
 }
 
-template <int NW, int TM, int TN, int NP, int STAGES, bool F16 = false, bool ONE = false>
+template <int NW, int TM, int TN, int NP, int STAGES, bool F16 = false, bool ONE = false, int KSF = 0>
 int launch(const ConvK& kp0, hipStream_t st) {
   constexpr int BM = NW * TM * 16, BN = TN * 16;
   ConvK kp = kp0;
@@ -460,10 +466,10 @@ int launch(const ConvK& kp0, hipStream_t st) {
   if constexpr (ONE) {
     if (kp.x2 || kp.x_planes) return PRPE_EINVAL;
     if (kp.in_scale)
-      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, true, true, false, false, true>), dim3(kp.nwg),
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, true, true, false, false, true, KSF>), dim3(kp.nwg),
                          dim3(NW * 64), 0, st, kp);
     else
-      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, false, false, true>), dim3(kp.nwg),
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, false, false, true, KSF>), dim3(kp.nwg),
                          dim3(NW * 64), 0, st, kp);
     return launch_status();
   }
@@ -591,9 +597,12 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
   if (prec == 4) {                                     // the precision-3 shapes, one fp16 plane
     // (no 256 x 128 / 64 x 128-wave tile: at two K-steps per iteration it spills)
     switch (tile) {
+      case 24: return launch<4, 2, 4, 2, 3, true, true>(kp, st);   // 128 x 64, wave 32 x 64
       case 25: return launch<8, 2, 4, 2, 3, true, true>(kp, st);   // 256 x 64, wave 32 x 64
       case 26: return launch<4, 2, 8, 2, 3, true, true>(kp, st);   // 128 x 128, 3 stages
       case 27: return launch<4, 2, 8, 2, 2, true, true>(kp, st);   // 128 x 128, 2 stages
+      case 28: return launch<4, 2, 8, 2, 2, true, true, 1>(kp, st);   // 27 at one K-step per iteration
+      case 29: return launch<4, 1, 8, 2, 2, true, true>(kp, st);   // 64 x 128, wave 16 x 128
       default: return PRPE_EINVAL;
     }
   }

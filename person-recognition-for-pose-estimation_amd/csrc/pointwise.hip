@@ -374,7 +374,7 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
     return h;
   };
   // ... tabulated once per block (one LDS read per output row in the loop instead of three and
-  // the selects; the row loop is VALU-bound: ~160 VALU per thread and row, profiles/r04_pmc_upconv.txt)
+  // the selects; the row loop is VALU-bound: ~160 VALU per thread and row, profiles/r04_pmc_upconv_conv.txt)
   for (int e = threadIdx.x; e < oy1 - oy0; e += 256) thi[e] = hi_at(oy0 + e);
   __syncthreads();
   int lo_row = Hi;

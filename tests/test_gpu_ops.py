@@ -473,6 +473,7 @@ GEMM_SHAPES = [
     (2, 64, 13, 11, 256),       # M = 286: one full + one ragged 256-row tile, 2 K-steps
     (3, 768, 8, 12, 768),       # ViT-like: K = 768, three column tiles
     (1, 96, 40, 40, 512),       # M = 1600, odd K-step count
+    (2, 32, 9, 9, 256),         # one K-step (the pipelined loop's prologue / tail only)
 ]
 
 

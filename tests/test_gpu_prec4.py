@@ -101,7 +101,7 @@ P4_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("tile", [0, 25, 26, 27])
+@pytest.mark.parametrize("tile", [0, 24, 25, 26, 27, 28, 29])
 @pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", P4_SHAPES)
 def test_conv_p4_matches_operand_emulation(B, Ci, H, W, Co, k, s, p, tile):
     x = torch.relu(rnd(B, Ci, H, W, seed=401)) * 7.0
@@ -119,7 +119,7 @@ def test_conv_p4_matches_operand_emulation(B, Ci, H, W, Co, k, s, p, tile):
     assert e_ref <= 2.0 ** -10, e_ref
 
 
-@pytest.mark.parametrize("tile", [0, 25, 27])
+@pytest.mark.parametrize("tile", [0, 24, 25, 27, 28, 29])
 @pytest.mark.parametrize("stride", [1, 2])
 def test_conv_p4_prologue_bound(tile, stride):
     """IR-50 res_layer: BN prologue on the input (in-bounds taps only), 3x3 conv, BN + PReLU.
@@ -164,6 +164,29 @@ def test_conv_p4_halo_bit_exact_vs_wave(B, Ci, H, W, Co, tile):
     assert torch.equal(a, b)
     emu, den = _emul(x, w, 1, 1, frame_amax(x), scale=sc, bias=bi, act="silu", res=r, res_mode=RES_PRE)
     assert ((a.double() - emu).abs() / (den + 1e-30)).max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("tile", [0, 30, 31, 34, 36, 37])
+@pytest.mark.parametrize("B,Ci,H,W,Co", [(2, 64, 17, 19, 96), (2, 128, 16, 16, 64), (1, 256, 14, 14, 256)])
+def test_conv_p4_halo_prologue_bit_exact_vs_wave(B, Ci, H, W, Co, tile):
+    """IR-50 res_layer on the haloed-tile kernel: the BN prologue is applied to the chunk's halo
+    as it is converted to fp16 (pixels inside the frame only; the padding stays 0), with the
+    activation scale from the prologue's bound -- bit-identical to the wave kernel's prologue
+    (tile 27), and within the operand emulation. tile 0: the automatic choice (the halo kernel
+    from 14 x 14 up)."""
+    x = rnd(B, Ci, H, W, seed=440) * 3.0
+    w = rnd(Co, Ci, 3, 3, seed=441, scale=1.0 / math.sqrt(Ci * 9))
+    in_s = rnd(Ci, seed=442) * 2.0
+    in_b = rnd(Ci, seed=443) * 4.0
+    sc = torch.rand(Co, generator=_g(444)) + 0.5
+    bi = rnd(Co, seed=445)
+    sl = torch.rand(Co, generator=_g(446)) * 0.3
+    kw = dict(in_s=in_s, in_b=in_b, act="prelu", scale=sc, bias=bi, slope=sl)
+    a = _conv_p4(x, w, 1, 1, tile=tile, **kw)
+    b = _conv_p4(x, w, 1, 1, tile=27, **kw)
+    assert torch.equal(a, b)
+    emu, den = _emul(x, w, 1, 1, frame_amax(x), in_s=in_s, in_b=in_b, scale=sc, bias=bi, act="prelu", slope=sl)
+    assert ((a.double() - emu).abs() / (den + 1e-30)).max().item() <= 2e-4
 
 
 def test_conv_p4_descriptor_rules():

@@ -39,6 +39,9 @@ SHAPES = {
     "ir50 output 7x7 512->512 @7 (M = frames)": (7, 7, 512, 512, 7, 1, 0),
     "ada_adapter.10 3x3 128->64 @112": (112, 112, 128, 64, 3, 1, 1),
     "ada body.0 3x3 64->64 @112": (112, 112, 64, 64, 3, 1, 1),
+    "ir50 body 3x3 64->64 @56": (56, 56, 64, 64, 3, 1, 1),
+    "ir50 body 3x3 128->128 @28": (28, 28, 128, 128, 3, 1, 1),
+    "ir50 body 3x3 512->512 @7": (7, 7, 512, 512, 3, 1, 1),
     "trunk l2 conv3 1x1 128->512 +res @80": (80, 80, 128, 512, 1, 1, 0, "res"),
 }
 
@@ -55,6 +58,8 @@ def main():
     ap.add_argument("--act", default="relu", help="epilogue activation (relu, gelu, silu, prelu, none)")
     ap.add_argument("--planes", action="store_true",
                     help="input in the planes format (x_planes; precision 0, wave-row kernel)")
+    ap.add_argument("--prologue", action="store_true",
+                    help="BN prologue on the input (in_scale / in_bias: the IR-50 res_layer's first conv)")
     ap.add_argument("--taps", type=int, default=0,
                     help="epilogue 1x1 GEMM to this many channels (prpe_conv_desc.w2; y not written)")
     a = ap.parse_args()
@@ -70,8 +75,9 @@ def main():
         for ko in [int(v) for v in a.korders.split(",")]:
             if ko == 1 and (k == 1 or Ci % 32):
                 continue
+            pro = dict(in_scale=torch.rand(Ci) + 0.5, in_bias=torch.rand(Ci) - 0.5) if a.prologue else {}
             pks[ko] = pack.pack_conv("b", w, s, p, dev, scale=torch.ones(Co), bias=torch.zeros(Co), act=a.act,
-                                     k_order=ko)
+                                     k_order=ko, **pro)
         Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
         y = torch.empty(B, Ho, Wo, Co, device=dev)
         r = torch.rand(B, Ho, Wo, Co, device=dev) if "res" in flags else None
@@ -82,7 +88,7 @@ def main():
           for prec in [int(v) for v in a.prec.split(",")]:
             for tile in [int(v) for v in a.tiles.split(",")]:
                 kw = dict(res=r, res_mode=1 if r is not None else 0, precision=prec, tile=tile, y_amax=ya,
-                          x_amax=xa if prec == 3 else None, x_planes=a.planes)
+                          x_amax=xa if prec in (3, 4) else None, x_planes=a.planes)
                 if a.taps:
                     kw["w2"] = torch.rand(a.taps, Co, device=dev) - 0.5
                     kw["y2"] = torch.empty(B, Ho, Wo, a.taps, device=dev)
@@ -99,7 +105,7 @@ def main():
                 e1.record()
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / a.iters
-                passes = {0: 3, 1: 1, 2: 6, 3: 3}[prec]
+                passes = {0: 3, 1: 1, 2: 6, 3: 3, 4: 1}[prec]
                 tf = fl / ms / 1e9
                 print(f"{name:40s} ko={ko} prec={prec} tile={tile} {ms:8.3f} ms  alg {tf:7.1f} TF/s  exec {tf * passes:7.1f} TF/s",
                       flush=True)
