@@ -558,8 +558,13 @@ bool conv_halo_eligible(const ConvK& kp, int prec, int km) {
 // much) takes it from 14 x 14 up whatever the waste: the IR-50 body's 14x14 256->256 -38 %,
 // 28x28 128->128 -21 %, 56x56 64->64 -30 % at bs = 256 (profiles/r04_conv_bench_ir50_halo.txt);
 // 7 x 7 stays on the wave kernel (one 8 x 16 tile per frame, 2.6x waste: no gain).
+// (PRPE_P4_HALO=0 in the environment restores the waste rule for precision 4: A/B runs)
 bool conv_halo_auto(const ConvK& kp, int prec) {
-  if (prec == 4 && kp.Ho >= 14 && kp.Wo >= 14) return true;
+  static const bool p4_halo = [] {
+    const char* e = getenv("PRPE_P4_HALO");
+    return !(e && e[0] == '0');
+  }();
+  if (prec == 4 && p4_halo && kp.Ho >= 14 && kp.Wo >= 14) return true;
   if (prec == 0 && !kp.x_planes) return false;
   const int tc = 16, tr = 8;
   const int64_t covered = (int64_t)((kp.Ho + tr - 1) / tr) * tr * ((kp.Wo + tc - 1) / tc) * tc;
