@@ -101,9 +101,12 @@ __device__ __forceinline__ void split_planes_f16(f4 v, float sa, unsigned long l
   for (int h = 0; h < 2; ++h) {
     const auto hi = __builtin_amdgcn_cvt_pkrtz(r[2 * h], r[2 * h + 1]);
     u[0][h] = __builtin_bit_cast(unsigned, hi);
-    r[2 * h] = sub_f32(r[2 * h], (float)hi[0]);
-    r[2 * h + 1] = sub_f32(r[2 * h + 1], (float)hi[1]);
-    u[1][h] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(r[2 * h], r[2 * h + 1]));
+    // r - hi straight from the packed fp16 halves (v_fma_mix_f32: -1 * f16 + f32, one VALU
+    // instead of v_cvt_f32_f16 + v_sub_f32; exact, as the remainder is representable in fp32)
+    float d0, d1;
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(d0) : "v"(u[0][h]), "v"(r[2 * h]));
+    asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(d1) : "v"(u[0][h]), "v"(r[2 * h + 1]));
+    u[1][h] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_pkrtz(d0, d1));
   }
 #pragma unroll
   for (int q = 0; q < 2; ++q) pl[q] = (unsigned long long)u[q][0] | ((unsigned long long)u[q][1] << 32);
