@@ -26,6 +26,7 @@ SHAPES = {
     "trunk stem 7x7/2 4->64 @640": (640, 640, 4, 64, 7, 2, 3),
     "trunk l1 1x1 256->64 @160": (160, 160, 256, 64, 1, 1, 0),
     "trunk l3 3x3 256->256 @40": (40, 40, 256, 256, 3, 1, 1),
+    "trunk l4 3x3 512->512 @20": (20, 20, 512, 512, 3, 1, 1),
     "trunk l3 1x1 1024->256 @40": (40, 40, 1024, 256, 1, 1, 0),
     "vit fc1 768->3072 (192 tok)": (16, 12, 768, 3072, 1, 1, 0),
     "vit fc2 3072->768 (192 tok)": (16, 12, 3072, 768, 1, 1, 0),
