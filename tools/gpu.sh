@@ -13,6 +13,7 @@
 #                                                FETCH_SIZE / WRITE_SIZE passes -> gpurun_out/TAG_traffic.json
 #   bash tools/gpu.sh py TAG SECONDS -- python-args...   any tool script -> gpurun_out/TAG.txt
 #   bash tools/gpu.sh evidence rNN               traffic records of the four configs, kernel trace, bench lines
+#                                                (= evidence_pmc rNN, then evidence_bench rNN)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 9
 O=gpurun_out
@@ -65,6 +66,10 @@ case "$cmd" in
     # end-of-round record on the committed sources: PMC traffic of every bench config's dominant
     # launch (profiles/rNN_pmc_traffic_<config>.json, read by bench.py while the sources match),
     # the kernel trace of the bench command, and the four bench lines with CPU baselines
+    # (evidence_pmc + evidence_bench: the same in two calls, each within one gpurun limit)
+    R=$1; [ -n "$R" ] || { echo "evidence needs the round tag (e.g. r04)"; exit 9; }
+    bash tools/gpu.sh evidence_pmc $R && bash tools/gpu.sh evidence_bench $R; exit $? ;;
+  evidence_pmc)
     R=$1; [ -n "$R" ] || { echo "evidence needs the round tag (e.g. r04)"; exit 9; }
     bash tools/gpu.sh traffic ${R}_full conv_halo 5000 14245036032 vit_pose.adapter.7 256 0 conv_halo.hip,conv.h,common.h \
       "3x3 256->128 @256x192, planes input, GELU, epilogue tap GEMM to 27 ch" -- tools/conv_bench.py --only vit_adapter.7 \
@@ -82,7 +87,9 @@ case "$cmd" in
     for C in full yolo_face vitpose yolo_raw; do
       mv $O/${R}_${C}_traffic.json $O/${R}_pmc_traffic_${C}.json && cp $O/${R}_pmc_traffic_${C}.json profiles/ || exit 15
     done
-    bash tools/gpu.sh trace ${R}_final || exit 16
+    bash tools/gpu.sh trace ${R}_final || exit 16 ;;
+  evidence_bench)
+    R=$1; [ -n "$R" ] || { echo "evidence needs the round tag (e.g. r04)"; exit 9; }
     for C in full yolo_face vitpose yolo_raw; do
       timeout -k 10 400 python bench.py --config $C --steps 20 --warmup 3 > $O/${R}_bench_${C}.json 2> $O/${R}_bench_${C}.err || exit 17
       tail -c 300 $O/${R}_bench_${C}.json
