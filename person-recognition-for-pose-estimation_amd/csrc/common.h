@@ -30,9 +30,13 @@ __device__ __forceinline__ f32x2v vexp2(f32x2v x) {
 }
 __device__ __forceinline__ float vrcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ f32x2v vrcp(f32x2v x) { return f32x2v{__builtin_amdgcn_rcpf(x[0]), __builtin_amdgcn_rcpf(x[1])}; }
-__device__ __forceinline__ float vsel_lt1(float a, float x, float y) { return a < 1.f ? x : y; }
-__device__ __forceinline__ f32x2v vsel_lt1(f32x2v a, f32x2v x, f32x2v y) {
-  return f32x2v{a[0] < 1.f ? x[0] : y[0], a[1] < 1.f ? x[1] : y[1]};
+__device__ __forceinline__ float vsel_lt(float a, float lim, float x, float y) { return a < lim ? x : y; }
+__device__ __forceinline__ float vsel_ge0(float a, float x, float y) { return a >= 0.f ? x : y; }
+__device__ __forceinline__ f32x2v vsel_ge0(f32x2v a, f32x2v x, f32x2v y) {
+  return f32x2v{a[0] >= 0.f ? x[0] : y[0], a[1] >= 0.f ? x[1] : y[1]};
+}
+__device__ __forceinline__ f32x2v vsel_lt(f32x2v a, float lim, f32x2v x, f32x2v y) {
+  return f32x2v{a[0] < lim ? x[0] : y[0], a[1] < lim ? x[1] : y[1]};
 }
 
 // exp(x) from the hardware base-2 exponential (v_exp_f32, 1 ulp) with x*log2(e) carried in
@@ -51,47 +55,37 @@ __device__ __forceinline__ T exp_hw_v(T x) {
 }
 __device__ __forceinline__ float exp_hw(float x) { return exp_hw_v<float>(x); }
 
-// erf(x) without branches (both pieces are evaluated; the select is per lane), ~24 VALU
-// instead of libm erff's two-branch form with a full expf (~45 VALU under divergence):
-//   |x| < 1 : x P(x^2), P of degree 5
-//   |x| >= 1: 1 - exp(Q(min(|x|, 4))), Q of degree 8 fitted to log(erfc) on [1, 4] (erf
-//             rounds to 1 in fp32 from |x| = 3.92 on)
-// least-squares fits made for this kernel (relative error of erf(x)/x, absolute error of
-// log erfc); max error 2.3 ulp over [-6, 6] in an fp32 emulation with exp_hw's 2 ulp, 1.5e-7
-// absolute. test_epilogue_activation_accuracy checks GELU through it against fp64.
-template <typename T>
-__device__ __forceinline__ T erf_fast_v(T x) {
-#pragma clang fp contract(off)
-  const T a = __builtin_elementwise_abs(x);
-  const T t = a * a;
-  T p = T(-0x1.26eecap-11f);
-  p = vfma(p, t, T(0x1.422d30p-8f));
-  p = vfma(p, t, T(-0x1.b59da6p-6f));
-  p = vfma(p, t, T(0x1.ce08bep-4f));
-  p = vfma(p, t, T(-0x1.812670p-2f));
-  p = vfma(p, t, T(0x1.20dd74p+0f));
-  const T ra = a * p;
-  const T b = __builtin_elementwise_min(a, T(4.f));
-  T q = T(0x1.b14578p-20f);
-  q = vfma(q, b, T(-0x1.7e711ep-15f));
-  q = vfma(q, b, T(0x1.36c82ep-11f));
-  q = vfma(q, b, T(-0x1.36a7bcp-8f));
-  q = vfma(q, b, T(0x1.aff5a4p-6f));
-  q = vfma(q, b, T(-0x1.c2788cp-4f));
-  q = vfma(q, b, T(-0x1.438d42p-1f));
-  q = vfma(q, b, T(-0x1.21529ap+0f));
-  q = vfma(q, b, T(0x1.3df11ep-12f));
-  const T rb = T(1.f) - exp_hw_v(q);
-  return __builtin_elementwise_copysign(vsel_lt1(a, ra, rb), x);
-}
-__device__ __forceinline__ float erf_fast(float x) { return erf_fast_v<float>(x); }
-
-// GELU and SiLU / sigmoid (the epilogue forms, see apply_act) for T = float or f32x2v
+// GELU(v) = v Phi(v) in ONE branch (round 4; before: 0.5 v (1 + erf(v / sqrt 2)) with a
+// two-piece erf, ~31 VALU): with b = min(|v| / sqrt 2, 4) and E = erfc(b) = exp(Q(b)),
+//   v >= 0: v - (v / 2) E        v < 0: (v / 2) E
+// Q(b) = b R(b), R of degree 10, a weighted least-squares fit of log erfc on [0, 4] made for this
+// kernel (Q(0) = 0 exactly, so E(0) = 1); ~24 VALU. fp32 emulation against fp64: <= 1.3 ulp
+// for |v| < 2, <= 15 ulp on [-4, -2] (the rounding of Q at |Q| ~ 8; the former erf form lost
+// ~400 ulp there to 1 + erf cancelling); past |v| = 5.66 the result is v or -0 (the fp32 CPU
+// reference gives -0 there too; the fp64 value is below 5e-8 in magnitude). erfc never cancels: the
+// positive branch subtracts at most half of v. test_epilogue_activation_accuracy checks it
+// against fp64.
 template <typename T>
 __device__ __forceinline__ T gelu_v(T v) {
 #pragma clang fp contract(off)
   const T h = T(0.5f) * v;
-  return vfma(h, erf_fast_v(v * T(0.70710678118654752440f)), h);
+  const T a = __builtin_elementwise_abs(v) * T(0.70710678118654752440f);
+  const T b = __builtin_elementwise_min(a, T(4.f));
+  T r = T(0x1.578a8cp-24f);
+  r = vfma(r, b, T(-0x1.19e418p-19f));
+  r = vfma(r, b, T(0x1.9b625ep-16f));
+  r = vfma(r, b, T(-0x1.5c96f4p-13f));
+  r = vfma(r, b, T(0x1.700bf2p-11f));
+  r = vfma(r, b, T(-0x1.b89b64p-10f));
+  r = vfma(r, b, T(0x1.37bf18p-14f));
+  r = vfma(r, b, T(0x1.3babe4p-6f));
+  r = vfma(r, b, T(-0x1.a53a7ap-4f));
+  r = vfma(r, b, T(-0x1.45f11cp-1f));
+  r = vfma(r, b, T(-0x1.20dd88p+0f));
+  // E = 0 past the fit (b clamped at 4): v - (v/2) erfc(4) rounds to v anyway, and v = inf stays
+  // inf instead of inf - inf
+  const T hE = h * vsel_lt(a, 4.f, exp_hw_v(r * b), T(0.f));
+  return vsel_ge0(v, v - hE, hE);
 }
 template <typename T>
 __device__ __forceinline__ T sigmoid_v(T v) {
@@ -101,7 +95,7 @@ __device__ __forceinline__ T sigmoid_v(T v) {
 
 // Activation applied in every epilogue, accurate to a few ulp of the fp32 CPU reference:
 // SiLU / sigmoid as v * rcp(1 + exp(-v)) (exp_hw, v_rcp_f32 1 ulp; ~10 VALU instead of the
-// ~25 of expf + an IEEE division), GELU with erf_fast.
+// ~25 of expf + an IEEE division), GELU in one branch (gelu_v).
 __device__ __forceinline__ float apply_act(float v, int act, float slope) {
   switch (act) {
     case PRPE_ACT_RELU: return v > 0.f ? v : 0.f;
