@@ -88,6 +88,9 @@ def q_w(w, scheme):
 
 GROUPS = {
     "trunk": lambda p: p.startswith("backbone."),
+    "trunk_l3": lambda p: p.startswith("backbone.layer3"),
+    "trunk_l4": lambda p: p.startswith("backbone.layer4"),
+    "trunk_l12": lambda p: p.startswith("backbone.layer1") or p.startswith("backbone.layer2"),
     "yolo_adapter": lambda p: ".adapter." in p and p.startswith("yolo_"),
     "yolo_net": lambda p: p.startswith("yolo_") and ".yolo." in p,
     "ada_adapter": lambda p: p.startswith("ada_face.adapter."),
