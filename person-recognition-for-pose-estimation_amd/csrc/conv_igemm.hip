@@ -766,8 +766,13 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const int t = e ? atoi(e) : 40;
     return t == 41 || t == 42 ? t : 40;
   }();
+  // PRPE_GEMM_MIN_KN=<n> keeps GEMMs with K * Co below n on the wave kernel (A/B runs)
+  static const int64_t gemm_min_kn = [] {
+    const char* e = getenv("PRPE_GEMM_MIN_KN");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
   if (tile == 0 && gemm_on && (kp.x_planes || (prec == 3 && gemm_p3)) && kp.M >= (1 << 15) &&
-      conv_gemm_eligible(kp, prec))
+      (int64_t)kp.K * kp.Co >= gemm_min_kn && conv_gemm_eligible(kp, prec))
     return conv_gemm_launch(kp, prec, gemm_tile, st);
   if (tile >= 30 && tile < 40)
     return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;
