@@ -104,6 +104,7 @@ GROUPS = {
     "vit_head": lambda p: p.startswith("vit_pose.vit_pose.head"),
     "vit_a7": lambda p: p.startswith("vit_pose.adapter.7"),          # the dominant 3x3 alone
     "yolo_a10": lambda p: p.startswith("yolo_face.adapter.10"),
+    "yolo_a7": lambda p: p.startswith("yolo_face.adapter.7"),
     "ada_a7": lambda p: p.startswith("ada_face.adapter.7"),
 }
 UPCONV = ("yolo_face.adapter.4", "yolo_person.adapter.4", "ada_face.adapter.4", "vit_pose.adapter.4",
