@@ -36,11 +36,12 @@ constexpr int GBK = 32;
 
 // F16: precision 3 (fp16 planes of the per-frame-scaled activations, the weights' fp16 planes
 // pre-scaled per output channel; the per-row inverse scale in the epilogue), as conv_wave.hip.
-template <int BN, int WM, int STAGES, bool APL, bool F16>
-__global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
+// BM = 128 (tile 43): 128 x 128 at 2 stages = 64 KB of LDS, two workgroups (16 waves) per CU
+template <int BN, int WM, int STAGES, bool APL, bool F16, int BM = 256>
+__global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK p) {
   static_assert(!(APL && F16), "planes input is precision 0");
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
-  constexpr int NW = 8, BM = 256, NP = 2;
+  constexpr int NW = 8, NP = 2;
   constexpr int WN = NW / WM;                          // waves along N
   constexpr int WTN = BN / WN;                         // wave tile (BM / WM) x WTN
   constexpr int TM = BM / WM / 16, TN = WTN / 16;
@@ -51,7 +52,7 @@ __global__ __launch_bounds__(512) void conv_gemm_kernel(ConvK p) {
   constexpr int PW = (NA + NBP) / NW;                  // pieces per wave and K-step
   static_assert((NA + NBP) % NW == 0, "pieces");
   constexpr int CS = WTN + 4;                          // epilogue row pitch (floats)
-  static_assert(NW * 16 * CS * 4 <= STAGE, "epilogue slab");
+  static_assert(NW * 16 * CS * 4 <= STAGES * STAGE, "epilogue slab");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -250,26 +251,28 @@ bool conv_gemm_eligible(const ConvK& kp, int prec) {
          !kp.in_scale && !kp.x2 && kp.xsw % 4 == 0;
 }
 
-template <int BN, int WM, int STAGES>
+template <int BN, int WM, int STAGES, int BM = 256>
 int launch_gemm(const ConvK& kp0, int prec, hipStream_t st) {
   if (kp0.Co % BN) return PRPE_EINVAL;
   ConvK kp = kp0;
   kp.tiles_n = kp.Co / BN;
-  const int64_t nwg = (int64_t)((kp.M + 255) / 256) * kp.tiles_n;
+  const int64_t nwg = (int64_t)((kp.M + BM - 1) / BM) * kp.tiles_n;
   if (nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
   const dim3 g(kp.nwg), b(512);
-  if (prec == 3) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, true>), g, b, 0, st, kp);
-  else if (kp.x_planes) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, true, false>), g, b, 0, st, kp);
-  else hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, false>), g, b, 0, st, kp);
+  if (prec == 3) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, true, BM>), g, b, 0, st, kp);
+  else if (kp.x_planes) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, true, false, BM>), g, b, 0, st, kp);
+  else hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, false, BM>), g, b, 0, st, kp);
   return launch_status();
 }
 
-// tile 40 = auto (256 x 128, 3 stages), 41 = 256 x 256 (2 stages), 42 = 256 x 128 (2 stages)
+// tile 40 = auto (256 x 128, 3 stages), 41 = 256 x 256 (2 stages), 42 = 256 x 128 (2 stages),
+// 43 = 128 x 128 (2 stages, two workgroups per CU)
 int conv_gemm_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
   switch (tile) {
     case 41: return launch_gemm<256, 2, 2>(kp, prec, st);
     case 42: return launch_gemm<128, 4, 2>(kp, prec, st);
+    case 43: return launch_gemm<128, 4, 2, 128>(kp, prec, st);
     default: return launch_gemm<128, 4, 3>(kp, prec, st);
   }
 }

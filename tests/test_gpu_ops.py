@@ -477,7 +477,7 @@ GEMM_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("tile", [40, 41, 42])
+@pytest.mark.parametrize("tile", [40, 41, 42, 43])
 @pytest.mark.parametrize("B,Ci,H,W,Co", GEMM_SHAPES)
 def test_conv_gemm_kernel_bit_exact_vs_wave(B, Ci, H, W, Co, tile):
     """conv_gemm.hip (256 x 256 tile, A and B both LDS-DMA'd) == the wave kernel bit for bit:
