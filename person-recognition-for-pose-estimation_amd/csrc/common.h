@@ -31,9 +31,9 @@ __device__ __forceinline__ f32x2v vexp2(f32x2v x) {
 __device__ __forceinline__ float vrcp(float x) { return __builtin_amdgcn_rcpf(x); }
 __device__ __forceinline__ f32x2v vrcp(f32x2v x) { return f32x2v{__builtin_amdgcn_rcpf(x[0]), __builtin_amdgcn_rcpf(x[1])}; }
 __device__ __forceinline__ float vsel_lt(float a, float lim, float x, float y) { return a < lim ? x : y; }
-__device__ __forceinline__ float vsel_ge0(float a, float x, float y) { return a >= 0.f ? x : y; }
-__device__ __forceinline__ f32x2v vsel_ge0(f32x2v a, f32x2v x, f32x2v y) {
-  return f32x2v{a[0] >= 0.f ? x[0] : y[0], a[1] >= 0.f ? x[1] : y[1]};
+__device__ __forceinline__ float vsel_lt0(float a, float x, float y) { return a < 0.f ? x : y; }
+__device__ __forceinline__ f32x2v vsel_lt0(f32x2v a, f32x2v x, f32x2v y) {
+  return f32x2v{a[0] < 0.f ? x[0] : y[0], a[1] < 0.f ? x[1] : y[1]};
 }
 __device__ __forceinline__ f32x2v vsel_lt(f32x2v a, float lim, f32x2v x, f32x2v y) {
   return f32x2v{a[0] < lim ? x[0] : y[0], a[1] < lim ? x[1] : y[1]};
@@ -82,10 +82,11 @@ __device__ __forceinline__ T gelu_v(T v) {
   r = vfma(r, b, T(-0x1.a53a7ap-4f));
   r = vfma(r, b, T(-0x1.45f11cp-1f));
   r = vfma(r, b, T(-0x1.20dd88p+0f));
-  // E = 0 past the fit (b clamped at 4): v - (v/2) erfc(4) rounds to v anyway, and v = inf stays
-  // inf instead of inf - inf
-  const T hE = h * vsel_lt(a, 4.f, exp_hw_v(r * b), T(0.f));
-  return vsel_ge0(v, v - hE, hE);
+  // (v/2) E = -0 past the fit (b clamped at 4): v - (v/2) erfc(4) rounds to v anyway. The select
+  // is on the product, so v = +-inf gives v - (-0) = +inf / -0 (not inf * 0 = NaN), and the branch
+  // test is v < 0, so a NaN takes the v - hE side and stays NaN
+  const T hE = vsel_lt(a, 4.f, h * exp_hw_v(r * b), T(-0.f));
+  return vsel_lt0(v, hE, v - hE);
 }
 template <typename T>
 __device__ __forceinline__ T sigmoid_v(T v) {

@@ -187,7 +187,7 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st);
 
 // haloed-tile 3x3 kernel (conv_halo.hip): 3x3 / s1 / p1, chunk-major weights, precision 0
 // (fp32 or planes input), 3 or 4; tile 30 = auto, 31..35 force a configuration.
-bool conv_halo_eligible(const ConvK& kp, int prec, int km);
+bool conv_halo_eligible(const ConvK& kp, int prec, int km, int tile = 30);   // tile: 30 (auto) or 31..37
 bool conv_halo_auto(const ConvK& kp, int prec);   // the automatic choice's shape rule
 
 // 256-row GEMM kernel (conv_gemm.hip) for 1x1 / s1 convs over contiguous pixels, Co % 128 == 0,

@@ -535,11 +535,15 @@ int launch_halo_taps(const ConvK& kp, int prec, hipStream_t st) {
 
 }  // namespace
 
-bool conv_halo_eligible(const ConvK& kp, int prec, int km) {
+bool conv_halo_eligible(const ConvK& kp, int prec, int km, int tile) {
   // 3x3 / stride 1 / pad 1 over whole 32-channel chunks (chunk-major weights), vectorised
-  // epilogue, precision 0 (fp32 or planes input) or 3 (fp16 planes + the input's max bound)
+  // epilogue, precision 0 (fp32 or planes input) or 3 (fp16 planes + the input's max bound).
+  // Precision 4's single-plane B ring needs whole LDS-DMA pieces per wave (launch_halo_kind:
+  // TN % NW == 0), which the forced 16 x 16-pixel 64-column tile (35) does not have; the
+  // automatic choice (30) never maps precision 4 there (34 / 36).
   const bool p3 = prec == 3 && kp.wh16 && kp.wl16 && kp.x_amax && !kp.x_planes;
-  const bool p4 = prec == 4 && kp.wh16 && kp.x_amax && !kp.x_planes && (!kp.in_scale || kp.in_bias);
+  const bool p4 = prec == 4 && kp.wh16 && kp.x_amax && !kp.x_planes && (!kp.in_scale || kp.in_bias) && tile != 35 &&
+                  !kp.w2;
   // buffer descriptors: one frame of x and one weight plane each < 2^31 bytes (32-bit offsets)
   const int64_t frame_bytes = ((int64_t)(kp.Hi - 1) * kp.xsh + (int64_t)(kp.Wi - 1) * kp.xsw + kp.Ci) * 4;
   const int64_t w_bytes = (int64_t)kp.k_pad * 2 * (((kp.Co + 127) / 128) * 128);

@@ -775,7 +775,7 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
       (int64_t)kp.K * kp.Co >= gemm_min_kn && conv_gemm_eligible(kp, prec))
     return conv_gemm_launch(kp, prec, gemm_tile, st);
   if (tile >= 30 && tile < 40)
-    return conv_halo_eligible(kp, prec, km) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;
+    return conv_halo_eligible(kp, prec, km, tile) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;
   if (tile == 0 && halo_on && conv_halo_auto(kp, prec) && conv_halo_eligible(kp, prec, km))
     return conv_halo_launch(kp, prec, 30, st);
   // precision 3 (split fp16) and 4 (one fp16 plane) are implemented by the wave-row kernel only

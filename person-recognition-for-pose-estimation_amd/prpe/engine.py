@@ -39,9 +39,27 @@ BN_EPS = 1e-5
 # YOLO net whose DFL box decode multiplies logit errors by the stride; the large adapters and
 # the ViT run the bf16 3-term split; the AdaFace branch (adapter + IR-50), whose embedding is
 # least sensitive to operand rounding (precision study: 1.8e-4 against the 1e-3 bar), runs one
-# fp16 term (round 4). PRPE_ADAFACE_PREC=0 restores the 3-term split there (A/B runs).
-AUTO_POLICY = {"trunk": 3, "yolo_adapter": 0, "yolo_net": 2, "vit": 0,
-               "adaface": int(os.environ.get("PRPE_ADAFACE_PREC", "4"))}
+# fp16 term (round 4). PRPE_ADAFACE_PREC=0 or 3 restores a 3-term split there (A/B runs); it is
+# read when an Engine is built (auto_policy), not at import.
+AUTO_POLICY = {"trunk": 3, "yolo_adapter": 0, "yolo_net": 2, "vit": 0, "adaface": 4}
+ADAFACE_PRECS = (0, 3, 4)
+
+
+def auto_policy() -> dict:
+    """AUTO_POLICY with the PRPE_ADAFACE_PREC override of the environment as it is now."""
+    pol = dict(AUTO_POLICY)
+    env = os.environ.get("PRPE_ADAFACE_PREC")
+    if env is not None:
+        try:
+            v = int(env)
+        except ValueError:
+            v = None
+        if v not in ADAFACE_PRECS:
+            raise ValueError(f"PRPE_ADAFACE_PREC={env!r}: expected one of {ADAFACE_PRECS}")
+        pol["adaface"] = v
+    return pol
+
+
 F16_PRECS = (3, 4)                  # precisions that read / keep per-frame max|x| slots
 AMAX_CHUNK = 1 << 16                # floats per chunk of a component's max|y| slot pool
 # PRPE_PLANES=0 keeps every activation in fp32 (A/B runs of the planes-format handoff)
@@ -92,9 +110,9 @@ class Engine:
         self.sd = state_dict
         self.device = torch.device(device)
         if precision == "auto":
-            self.policy = dict(AUTO_POLICY)
+            self.policy = auto_policy()
         elif isinstance(precision, dict):
-            self.policy = dict(AUTO_POLICY, **precision)
+            self.policy = dict(auto_policy(), **precision)
         else:
             self.policy = {k: int(precision) for k in AUTO_POLICY}
         self.precision = 0
@@ -187,8 +205,10 @@ class Engine:
     def _f16_ok(x, p: ConvPack, out, res=None, prologue=False):
         """``prologue``: an input-side affine is allowed (precision 4 bounds it in-kernel)."""
         chunked = p.k_order == 1 or (p.kh * p.kw == 1 and p.ci % 32 == 0)
+        # (a planes-format input is read by precision 0 only: its consumer drops to 0 as well)
         return (chunked and (prologue or p.in_scale is None) and x.stride(3) == 1 and x.data_ptr() % 16 == 0 and
-                Engine._vec4(out) and Engine._vec4(res) and getattr(x, "_prpe_amax", None) is not None)
+                Engine._vec4(out) and Engine._vec4(res) and getattr(x, "_prpe_amax", None) is not None and
+                not getattr(x, "_prpe_planes", False))
 
     def pk_dual(self, q) -> ConvPack:
         """Bottleneck ``q`` (block 0 of a stage): relu(bn3(conv3(o)) + bn_ds(downsample(x))) as
@@ -231,7 +251,10 @@ class Engine:
         x_planes = getattr(x, "_prpe_planes", False)
         if x_planes and prec != 0:
             raise RuntimeError(f"{p.name}: planes-format input needs precision 0, got {prec}")
-        y_planes = PLANES_ON and planes_out and prec == 0 and p.co % 8 == 0 and out.is_contiguous()
+        # planes output only where the component itself runs precision 0 (as upconv(): inside a
+        # precision-3/4 scope a conv that fell back to 0 keeps fp32 output for its f16 consumers)
+        y_planes = (PLANES_ON and planes_out and prec == 0 and self.precision == 0 and p.co % 8 == 0 and
+                    out.is_contiguous())
         kw = dict(res=res, res_mode=res_mode, act=act, precision=prec, tile=p.tile, x_amax=xa, y_amax=ya, x2=x2,
                   x2_amax=x2_amax if prec == 3 else None, x_planes=x_planes, y_planes=y_planes, w2=w2, y2=y2,
                   **stage2)

@@ -104,10 +104,9 @@ def test_config2_yolo_face_bs64(model, state_dict):
     print("config 2 end-to-end NMS match rate vs the oracle's detections:", rates)
     # end to end, NMS runs on OUR scores, which differ from the oracle's by up to ~3e-5 (measured):
     # a pair whose suppression decision is tied to that level (IoU within rounding of 0.65, or two
-    # scores that swap order) may legitimately flip, so a few of up to 300 kept rows per frame may
-    # differ without any regression (the bit-exact NMS check on the same tensor is the loop above).
-    # Measured 1.0 on every frame in rounds 3-4.
-    assert min(rates) >= 0.98
+    # scores that swap order) could legitimately flip. Measured 1.0 on every frame in rounds 3-5,
+    # so the test keeps the exact match: a flip must be looked at, not absorbed by a threshold.
+    assert min(rates) == 1.0, rates
 
 
 def test_config3_vitpose_from_pixels_vs_transformers_golden(model):

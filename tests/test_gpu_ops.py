@@ -876,6 +876,32 @@ def test_epilogue_activation_accuracy(act):
     assert not bad.any(), (v[bad][:8], got[bad][:8], ref[bad][:8])
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("act", ["silu", "sigmoid", "gelu"])
+def test_epilogue_activation_inf_nan(act):
+    """apply_act at +-inf and NaN: +inf gives the activation's limit (SiLU / GELU +inf, sigmoid
+    1; torch's CPU GELU gives NaN there), a NaN stays NaN, and -inf gives the limit 0 or, where
+    the fp32 CPU reference computes -inf * 0 = NaN (SiLU), NaN as well. Each special value
+    sits on its own pixel with zero neighbours (at unit scale the bilinear weights of the
+    neighbours are 0, and 0 * inf would make THEM NaN -- a property of the harness, not of the
+    epilogue)."""
+    vals = [float("inf"), float("-inf"), float("nan")]
+    H = W = 8
+    z = torch.zeros(1, H, W, 9 * 4)
+    pos = [(1, 1), (1, 4), (4, 1)]
+    for (i, j), v in zip(pos, vals):
+        z[0, i, j, 4 * 4] = v                   # tap (dy=1, dx=1), channel 0
+    y = torch.empty(1, H, W, 4, device=DEV)
+    ops.upconv3x3(z.to(DEV), y, True, torch.ones(4, device=DEV), torch.zeros(4, device=DEV), None, act)
+    torch.cuda.synchronize()
+    got = [y[0, i, j, 0].item() for i, j in pos]
+    ref = {"silu": F.silu, "sigmoid": torch.sigmoid, "gelu": F.gelu}[act](torch.tensor(vals)).tolist()
+    lim = {"silu": (math.inf, 0.0), "sigmoid": (1.0, 0.0), "gelu": (math.inf, 0.0)}[act]
+    assert got[0] == lim[0], (got, ref)
+    assert got[1] == lim[1] or (math.isnan(ref[1]) and math.isnan(got[1])), (got, ref)
+    assert math.isnan(got[2]), got
+
+
 @pytest.mark.parametrize("hi,wi,ho,wo,ac", [(20, 20, 160, 160, True), (20, 20, 256, 192, True),
                                         (16, 12, 64, 48, False), (7, 9, 20, 13, False), (20, 20, 23, 21, True),
                                         (20, 20, 112, 112, True), (9, 5, 40, 17, False), (13, 6, 37, 11, True),

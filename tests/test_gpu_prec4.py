@@ -203,6 +203,12 @@ def test_conv_p4_descriptor_rules():
         ops.conv2d(x, pk, y, precision=4, x_amax=xa, x2=x, x2_amax=xa)
     ops.conv2d(x, pk, y, precision=4, x_amax=xa)
     torch.cuda.synchronize()
+    # the haloed-tile kernel's forced 16 x 16-pixel 64-column tile has no single-plane form
+    pk3 = pack.pack_conv("r3", rnd(64, 64, 3, 3, seed=432), 1, 1, DEV, k_order=1)
+    with pytest.raises(Exception):
+        ops.conv2d(x, pk3, y, precision=4, x_amax=xa, tile=35)
+    ops.conv2d(x, pk3, y, precision=4, x_amax=xa, tile=34)
+    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("act", ["prelu", "gelu", "silu"])

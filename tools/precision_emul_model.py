@@ -13,6 +13,12 @@ Operand schemes (per layer group):
   f16w   weights one plane, activations two planes: 2 terms
   bf16   one bf16 plane each (RNE): 1 term
   bf16x3 two bf16 planes each, 3 terms (today's precision 0)
+  f16x3  two scaled fp16 planes each, 3 terms (precision 3)
+
+    --seed N              weight seed of the synthetic net (prpe.synth; default its WEIGHT_SEED)
+    --ada-gamma LO,HI     redraw the IR-50 residual-branch tail gammas (res_layer.5) from U(LO, HI)
+                          instead of the tamed U(0.05, 0.25): the precision-4 robustness check of
+                          round 5 (profiles/r05_precision4_robustness.txt)
 For the upsample->conv3x3 layers the GPU's GEMM operand is the LOW-resolution tensor (tap
 rewrite), so the activation rounding is applied before the interpolation.
 """
@@ -60,6 +66,8 @@ def q_act(x, scheme):
     if scheme == "bf16x3":
         h = _rbf(x)
         return h + _rbf(x - h)      # the 3-term product drops lo*lo: emulated at operand level
+    if scheme == "f16x3":
+        return q_act(x, "f16w")
     return x
 
 
@@ -71,7 +79,7 @@ def q_w(w, scheme):
         e = torch.where(m > 0, 15 - e, torch.zeros_like(e))
         s = torch.ldexp(torch.ones_like(m), e).view(-1, *([1] * (w.dim() - 1)))
         return _rne16(w * s) / s
-    if scheme == "f16a":
+    if scheme in ("f16a", "f16x3"):
         m = w.abs().flatten(1).amax(1)
         _, e = torch.frexp(m)
         e = torch.where(m > 0, 15 - e, torch.zeros_like(e))
@@ -228,10 +236,22 @@ def parse_policy(s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=2)
+    ap.add_argument("--seed", type=int, default=None)
+    ap.add_argument("--ada-gamma", default=None)
     ap.add_argument("policies", nargs="*", default=["all=bf16x3", "all=f16"])
     a = ap.parse_args()
     torch.set_num_threads(os.cpu_count() or 8)
-    sd = synth.make_state_dict(arch.state_dict_spec())
+    seed = synth.WEIGHT_SEED if a.seed is None else a.seed
+    sd = synth.make_state_dict(arch.state_dict_spec(), seed=seed)
+    if a.ada_gamma:
+        lo, hi = (float(v) for v in a.ada_gamma.split(","))
+        n = 0
+        for k in list(sd):
+            if k.startswith("ada_face.adaface_model.") and k.endswith("res_layer.5.weight"):
+                sd[k] = synth.uniform(seed + 7, k, tuple(sd[k].shape), lo, hi)
+                n += 1
+        print(f"# IR-50 residual-branch gammas redrawn from U({lo}, {hi}): {n} tensors", flush=True)
+    print(f"# weight seed {seed}, {a.frames} frames", flush=True)
     x = synth.frames(a.frames)
     with torch.no_grad():
         ref = R.forward_all(sd, x)
@@ -243,6 +263,7 @@ def main():
         c, _ = R.keypoints_from_heatmaps(o["heatmaps"])
         print(f"{s:60s} heat {float((o['heatmaps'] - ref['heatmaps']).abs().max()):.2e} "
               f"emb {float((o['emb'] - ref['emb']).abs().max()):.2e} "
+              f"emb-norm/rel {float(((o['norm'] - ref['norm']).abs() / ref['norm'].abs()).max()):.1e} "
               f"cls {float((o['det'][:, 4] - ref['det'][:, 4]).abs().max()):.2e} "
               f"box/max {float((o['det'][:, :4] - ref['det'][:, :4]).abs().max() / rb):.2e} "
               f"oks {R.oks_delta(c, rc):.1e}  ({time.time() - t0:.0f}s)", flush=True)
