@@ -571,6 +571,220 @@ __global__ __launch_bounds__(NWAVE * 64) void vit_attention_s_kernel(const float
   }
 }
 
+// ----------------------------------------------------------------------------- v4
+// vit_attention_h_kernel (round 5) -- whole heads: a workgroup owns `hpw` heads of one frame and
+// stages each head's K and V^T for ALL 192 keys once (split-bf16 planes, 110 KB of LDS), so a
+// head costs two barriers (v3: two per 64-key chunk, six per head) and the softmax runs over two
+// 96-key halves in registers (one online merge; the whole row would be 48 score registers per lane
+// and spill beside the next head's prefetch). The
+// fp32 K / V of head h + 1 are loaded into registers while head h computes (issued right after
+// head h's staging, consumed by the next staging; Q at the top of its own head), so the HBM
+// reads -- the kernel's bound:
+// q, k, v read once, o written once -- overlap the MFMAs. Products as v3 (3 bf16 terms for S and
+// for PV, transposed: S^T = K Q^T, O^T = V^T P^T with P taken straight from the S^T accumulators).
+template <bool OPL>
+__global__ __launch_bounds__(NWAVE * 64) void vit_attention_h_kernel(const float* __restrict__ qkv, AttnStrides sd,
+                                                                    float* __restrict__ out, int H, int hpw,
+                                                                    float scale) {
+  constexpr int NT = NWAVE * 64;
+  constexpr int KT = AL / 16;                             // 12 key tiles
+  constexpr int VR = AL + 8;                              // bf16 per V^T row (pad 16 B: conflict-free 8-B reads)
+  constexpr int KSZ = AL * KROW, VSZ = AD * VR;
+  constexpr int KN = AL * (AD / 4);                       // float4 of K per head: 3072
+  constexpr int VN = (AL / 4) * (AD / 4);                 // 4 keys x 4 channels V items: 768
+  constexpr int KPT = KN / NT, VPT = VN / NT;             // 4, 1 per thread
+  static_assert(KN % NT == 0 && VN % NT == 0, "whole items per thread");
+  __shared__ __attribute__((aligned(16))) __bf16 lds[2 * KSZ + 2 * VSZ];
+  __bf16* Kh = lds;
+  __bf16* Kl = lds + KSZ;
+  __bf16* Vh = lds + 2 * KSZ;
+  __bf16* Vl = lds + 2 * KSZ + VSZ;
+
+  const int groups = H / hpw;
+  const int b = blockIdx.x / groups, h0 = (blockIdx.x % groups) * hpw;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fg = lane >> 4;
+  const int64_t rs = sd.tok;
+  const float* base = qkv + (int64_t)b * sd.frame;
+  const int q0 = wave * 16;
+
+  // the frame's q / k / v through one buffer descriptor: ONE 32-bit per-thread offset per operand
+  // kind, the head / key-block / kk parts as scalar offsets (64-bit per-item pointers needed ~40
+  // VGPRs beside the prefetch registers and spilled)
+  const int frame_bytes = (int)(((int64_t)(AL - 1) * rs + 2 * sd.which + (int64_t)(H - 1) * sd.head + AD) * 4);
+  const __amdgpu_buffer_rsrc_t fr_rsrc = buf_rsrc(base, frame_bytes);
+  const unsigned kvo = (unsigned)(((int64_t)(tid / (AD / 4)) * rs + (tid % (AD / 4)) * 4) * 4);      // K item j: + 48 j keys
+  const unsigned vvo = (unsigned)(((int64_t)(tid / (AD / 4)) * 4 * rs + (tid % (AD / 4)) * 4) * 4);  // V item: keys 4 k4 + kk
+  const unsigned qvo = (unsigned)(((int64_t)(q0 + fr) * rs + fg * 8) * 4);
+  static_assert(KPT * NT / (AD / 4) == AL && VPT == 1, "item maps");
+  f32x4 kr[KPT], vr[VPT][4], qr[4];   // native vectors (arrays of HIP float4 structs go to scratch)
+  auto ld4 = [&](unsigned vo, int64_t so) {
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(fr_rsrc, vo, (int)so, 0));
+  };
+  auto fetch = [&](int hh) {
+    const int64_t hb = (int64_t)hh * sd.head * 4;
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) kr[j] = ld4(kvo, hb + sd.which * 4 + (int64_t)j * (NT / (AD / 4)) * rs * 4);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) vr[0][kk] = ld4(vvo, hb + 2 * sd.which * 4 + (int64_t)kk * rs * 4);
+  };
+  // the wave's 16 queries of head hh: loaded at the top of the head's iteration (their latency
+  // runs under the first barrier and the staging), so they are not live across the MFMAs
+  auto fetch_q = [&](int hh) {
+    const int64_t hb = (int64_t)hh * sd.head * 4;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      qr[2 * ks] = ld4(qvo, hb + ks * 128);
+      qr[2 * ks + 1] = ld4(qvo, hb + ks * 128 + 16);
+    }
+  };
+  auto stage = [&]() {
+#pragma unroll
+    for (int j = 0; j < KPT; ++j) {
+      const int i = tid + j * NT;
+      const int key = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+      const float kv[4] = {kr[j][0], kr[j][1], kr[j][2], kr[j][3]};
+      bf16x4 khi, klo;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        __bf16 hi, lo;
+        split_bf16(kv[e], hi, lo);
+        khi[e] = hi; klo[e] = lo;
+      }
+      *reinterpret_cast<bf16x4*>(Kh + key * KROW + d4) = khi;
+      *reinterpret_cast<bf16x4*>(Kl + key * KROW + d4) = klo;
+    }
+#pragma unroll
+    for (int j = 0; j < VPT; ++j) {
+      const int i = tid + j * NT;
+      const int k4 = i / (AD / 4), d4 = (i % (AD / 4)) * 4;
+#pragma unroll
+      for (int dd = 0; dd < 4; ++dd) {
+        bf16x4 vhi, vlo;
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          __bf16 hi, lo;
+          split_bf16(vr[j][kk][dd], hi, lo);
+          vhi[kk] = hi; vlo[kk] = lo;
+        }
+        *reinterpret_cast<bf16x4*>(Vh + (d4 + dd) * VR + k4 * 4) = vhi;
+        *reinterpret_cast<bf16x4*>(Vl + (d4 + dd) * VR + k4 * 4) = vlo;
+      }
+    }
+  };
+
+  fetch(h0);
+  for (int it = 0; it < hpw; ++it) {
+    const int hh = h0 + it;
+    fetch_q(hh);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();                                     // head it - 1's K / V reads retired
+    __builtin_amdgcn_sched_barrier(0);
+    stage();
+    // the next head's K / V, in flight across this head's MFMAs. Unconditional (the last head
+    // re-reads its own, unused): behind a branch, the compiler's waits for the Q loads merged both
+    // paths and drained this prefetch (vmcnt(0)) before the MFMAs
+    fetch(it + 1 < hpw ? hh + 1 : hh);
+    bf16x8 qh[2], ql[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const float v[8] = {qr[2 * ks][0], qr[2 * ks][1], qr[2 * ks][2], qr[2 * ks][3],
+                          qr[2 * ks + 1][0], qr[2 * ks + 1][1], qr[2 * ks + 1][2], qr[2 * ks + 1][3]};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __bf16 hi, lo;
+        split_bf16(v[j], hi, lo);
+        qh[ks][j] = hi; ql[ks][j] = lo;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    __builtin_amdgcn_sched_barrier(0);
+
+    // two halves of 96 keys (register budget: 24 score registers per lane instead of 48), one
+    // online-softmax merge between them: S^T tiles rows = keys 16 t + 4 fg + r, column = query
+    // q0 + fr
+    float m = -1e30f, sum = 0.f;                         // finite: exp_hw(-inf) would be NaN
+    f32x4 o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int hf = 0; hf < 2; ++hf) {
+      constexpr int HT = KT / 2;
+      f32x4 sc[HT];
+#pragma unroll
+      for (int t = 0; t < HT; ++t) {
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          const int off = ((hf * HT + t) * 16 + fr) * KROW + ks * 32 + fg * 8;
+          const bf16x8 kh = *reinterpret_cast<const bf16x8*>(Kh + off);
+          const bf16x8 kl = *reinterpret_cast<const bf16x8*>(Kl + off);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kl, qh[ks], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, ql[ks], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kh, qh[ks], acc, 0, 0, 0);
+        }
+        sc[t] = acc;
+        // (keeps the compiler from hoisting every tile's K fragment reads ahead of the MFMAs)
+        if (t % 2 == 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { sc[t][r] *= scale; mx = fmaxf(mx, sc[t][r]); }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m, mx);
+      const float alpha = exp_hw(m - mn);                // 0 for the first half
+      m = mn;
+      float hs = 0.f;
+#pragma unroll
+      for (int t = 0; t < HT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { const float e = exp_hw(sc[t][r] - mn); sc[t][r] = e; hs += e; }
+      hs += __shfl_xor(hs, 16, 64);
+      hs += __shfl_xor(hs, 32, 64);
+      sum = sum * alpha + hs;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) o[j] *= alpha;
+      // O^T += V^T P^T, 32 keys per step
+#pragma unroll
+      for (int cc = 0; cc < HT / 2; ++cc) {
+        bf16x8 ph, pl;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          __bf16 hi, lo;
+          split_bf16(sc[2 * cc + (jj >> 2)][jj & 3], hi, lo);
+          ph[jj] = hi; pl[jj] = lo;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int off = (j * 16 + fr) * VR + hf * (AL / 2) + cc * 32 + fg * 4;
+          const bf16x4 a0 = *reinterpret_cast<const bf16x4*>(Vh + off);
+          const bf16x4 a1 = *reinterpret_cast<const bf16x4*>(Vh + off + 16);
+          const bf16x4 b0 = *reinterpret_cast<const bf16x4*>(Vl + off);
+          const bf16x4 b1 = *reinterpret_cast<const bf16x4*>(Vl + off + 16);
+          const bf16x8 vh = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+          const bf16x8 vl = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+          o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vl, ph, o[j], 0, 0, 0);
+          o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, pl, o[j], 0, 0, 0);
+          o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vh, ph, o[j], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    const float inv = __builtin_amdgcn_rcpf(sum);
+    float* prow = out + ((int64_t)b * AL + q0 + fr) * (H * AD);
+    const int c0 = hh * AD + fg * 4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (OPL) store_planes4(reinterpret_cast<uint16_t*>(prow), c0 + j * 16, o[j] * inv);
+      else *reinterpret_cast<f32x4*>(prow + c0 + j * 16) = o[j] * inv;
+    }
+  }
+}
+
 // ----------------------------------------------------------------------------- PSA
 __device__ __forceinline__ int64_t voff(const prpe_view& v, int n, int hh, int ww, int c) {
   return (int64_t)n * v.sn + (int64_t)hh * v.sh + (int64_t)ww * v.sw + (int64_t)c * v.sc;
@@ -687,10 +901,11 @@ int attention_launch(const float* qkv, AttnStrides sd, float* out, int32_t B, in
   // PRPE_ATTN selects the kernel for A/B runs: 1 = the round-1 kernel (P through LDS, all 192
   // keys staged, 12 waves), KC*10 + QT = transposed kernel with KC-key chunks and QT query tiles
   // per wave (322, 641, 642, 962); 32 / 64 / 96 = the streaming kernel with that chunk;
-  // default 64. Only the streaming kernel takes strided (e.g. head-major) operands.
+  // 4 = the whole-head kernel (v4, round 5); default 4. The streaming and whole-head kernels take
+  // strided (e.g. head-major) operands.
   static const int sel = [] {
     const char* e = getenv("PRPE_ATTN");
-    return e ? atoi(e) : 64;
+    return e ? atoi(e) : 4;
   }();
   const bool rowmajor = sd.frame == (int64_t)L * 3 * H * D && sd.which == (int64_t)H * D && sd.head == D &&
                         sd.tok == (int64_t)3 * H * D;
@@ -703,7 +918,12 @@ int attention_launch(const float* qkv, AttnStrides sd, float* out, int32_t B, in
   const dim3 gs(B * H / hpw);
   if (out_planes) {
     if ((uintptr_t)out % 32) return PRPE_EINVAL;
-    hipLaunchKernelGGL((vit_attention_s_kernel<64, true>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale);
+    if (sel == 4) hipLaunchKernelGGL((vit_attention_h_kernel<true>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale);
+    else hipLaunchKernelGGL((vit_attention_s_kernel<64, true>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale);
+    return launch_status();
+  }
+  if (sel == 4) {
+    hipLaunchKernelGGL((vit_attention_h_kernel<false>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale);
     return launch_status();
   }
   switch (rowmajor ? sel : 64) {

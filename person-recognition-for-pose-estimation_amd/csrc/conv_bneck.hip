@@ -54,11 +54,8 @@ struct BneckK {
 namespace {
 
 constexpr int BK_ = 32;
-constexpr int TR = 8, TC = 16, NW = 8;
-constexpr int HW_ = TC + 2, HP = (TR + 2) * HW_;        // 18, 180 haloed pixels
-constexpr int NRB1 = (HP + 15) / 16;                     // 12 row blocks of haloed pixels
-constexpr int CHB1 = NRB1 * 16 * 128;                    // bytes of one 32-channel chunk of t1
-constexpr int CHB2 = TR * TC * 128;                      // ... of t2
+constexpr int TC = 16;                                   // tile columns (one 16-pixel row block per wave)
+constexpr int HW_ = TC + 2;                              // 18 haloed columns
 constexpr int W3_PART = 32 * 1024;                       // one W3 part (below) in the overlay
 constexpr int RING = 4;                                  // W1 / W2 ring stages (3 K-steps of lookahead)
 
@@ -70,8 +67,16 @@ constexpr int RING = 4;                                  // W1 / W2 ring stages 
 // LDS: TT (t1, then t2 in its first (MID/32) CHB2 bytes), then the W1 / W2 ring; a W3 part
 // overlays TT past t2 (and, at MID 64, ring stages 0-1). MID 64: 48 + 32 = 80 KB, two
 // workgroups per CU; MID 128: 96 + 64 = 160 KB, one.
-template <int MIDT, bool PROJ> struct BShape {
+// TRT = output rows of the tile = waves of the workgroup (8: 8 x 16 pixels, 8 waves; 16 (MID 64
+// only, round 5): 16 x 16 pixels, 16 waves, one workgroup per CU -- every weight byte staged
+// into LDS serves twice the pixels, and the 3x3 halo is 1.27x the tile instead of 1.41x).
+template <int MIDT, bool PROJ, int TRT = 8> struct BShape {
   static constexpr int MID = MIDT, CIO = 4 * MIDT;
+  static constexpr int TR = TRT, NW = TRT;
+  static constexpr int HP = (TR + 2) * HW_;               // 180 / 324 haloed pixels
+  static constexpr int NRB1 = (HP + 15) / 16;             // 12 / 21 row blocks of haloed pixels
+  static constexpr int CHB1 = NRB1 * 16 * 128;            // bytes of one 32-channel chunk of t1
+  static constexpr int CHB2 = TR * TC * 128;              // ... of t2
   static constexpr int CIN = PROJ ? MID : CIO;           // x channels
   static constexpr int NK1 = CIN / BK_;                  // phase-1 K-steps
   static constexpr int NKS3 = PROJ ? 2 * MID / BK_ : MID / BK_;   // phase-3 K-steps
@@ -80,7 +85,13 @@ template <int MIDT, bool PROJ> struct BShape {
   static constexpr int W3_STEP = 2 * R3 * 64;            // one K-step of a part (both planes)
   static constexpr int TT_BYTES = (MID / 32) * CHB1;
   static constexpr int STAGE = 2 * MID * 64;             // one K-step of W1 / W2 (both planes)
-  static constexpr int PPW = STAGE / 1024 / NW;          // its LDS-DMA pieces per wave
+  // its LDS-DMA pieces per wave: whole 1-KiB pieces (16 weight rows x 64 B), or -- 16 waves on
+  // an 8-KiB stage -- ONE half piece per wave (lanes 0-31, 8 rows): every wave issues the same
+  // number of DMA instructions per K-step, so the counted waits below are the same for all
+  static constexpr bool HALF = STAGE / 1024 < NW;
+  static constexpr int PPW = HALF ? 1 : STAGE / 1024 / NW;
+  static constexpr int PROWS = HALF ? 8 : 16;            // weight rows per piece
+  static constexpr int PW3 = 32 / NW;                    // W3 pieces (1 KiB) per wave and part
   static constexpr int RING_OFF = TT_BYTES;
   static constexpr int W3_OFF = (MID / 32) * CHB2;       // after t2
   static constexpr int LDS_BYTES = TT_BYTES + RING * STAGE;
@@ -89,9 +100,10 @@ template <int MIDT, bool PROJ> struct BShape {
   // stages 0-1): part h + 1 is then DMA'd under part h's MFMAs instead of after them
   static constexpr bool W3DB = W3_OFF + 2 * W3_PART <= RING_OFF + 2 * STAGE;
   static_assert(!PROJ || MID == 64, "projection block: layer1.0 only");
-  static_assert(PPW >= 1 && STAGE == PPW * NW * 1024, "W ring pieces");
+  static_assert(PPW >= 1 && STAGE == PPW * NW * PROWS * 64, "W ring pieces");
   static_assert(NKS3 * W3_STEP == W3_PART, "W3 part size");
-  static_assert(NKS3 * 2 * (R3 / 16) == 4 * NW, "4 W3 pieces per wave and part");
+  static_assert(NKS3 * 2 * (R3 / 16) == PW3 * NW && PW3 >= 1, "whole W3 pieces per wave and part");
+  static_assert(TR == 8 || (TR == 16 && MID == 64), "16-row tile: inner width 64 only (LDS)");
   static_assert(W3_OFF + W3_PART <= RING_OFF + 2 * STAGE, "W3 part overlay below ring stage 2");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 };
@@ -134,11 +146,13 @@ __device__ __forceinline__ f32x4 mfma3t(const f16x8 (&w)[2], const f16x8 (&a)[2]
 
 // launch bound: HIP's second argument is waves per SIMD, so WPC workgroups of NW waves per CU =
 // WPC * NW / 4 (caps VGPRs at 128 for the 80-KB shapes; measured neutral, tools/run_r03ac.sh)
-template <int MIDT, bool PROJ>
-__global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void bneck_kernel(BneckK p) {
-  using S = BShape<MIDT, PROJ>;
+template <int MIDT, bool PROJ, int TRT>
+__global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4)) void bneck_kernel(BneckK p) {
+  using S = BShape<MIDT, PROJ, TRT>;
   constexpr int MID = S::MID, CIO = S::CIO, CIN = S::CIN, NK1 = S::NK1, R3 = S::R3, W3_STEP = S::W3_STEP;
   constexpr int STAGE = S::STAGE, PPW = S::PPW, RING_OFF = S::RING_OFF, W3_OFF = S::W3_OFF;
+  constexpr int TR = S::TR, NW = S::NW, HP = S::HP, NRB1 = S::NRB1, CHB1 = S::CHB1, CHB2 = S::CHB2;
+  constexpr int PROWS = S::PROWS, PW3 = S::PW3;
   constexpr int NJ1 = MID / 16;                              // 16-channel column blocks of t1 / t2
   __shared__ __attribute__((aligned(1024))) unsigned char lds[S::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -161,25 +175,31 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void b
     wr[l][0] = buf_rsrc(p.wh[l], rows * p.kp[l] * 2);
     wr[l][1] = buf_rsrc(p.wl[l], rows * p.kp[l] * 2);
   }
-  // W1 / W2 ring pieces of this wave: piece j = wave PPW + i -> plane j / NJ1 (= the wave's
-  // plane: waves 0-3 the hi plane, 4-7 the lo), rows 16 (j % NJ1) .. +16. The plane's descriptors
-  // are selected once (wave-uniform SGPRs: a per-piece select spilled them to scratch)
-  static_assert(NJ1 % PPW == 0 && PPW * NW == 2 * NJ1, "W ring piece map");
-  const bool bq = wave * PPW / NJ1 != 0;
+  // W1 / W2 ring pieces of this wave: piece j = wave PPW + i -> plane j / NPP (= the wave's
+  // plane: the first half of the waves the hi plane, the second the lo), rows PROWS (j % NPP) ..
+  // + PROWS (NPP = MID / PROWS pieces per plane). The plane's descriptors are selected once
+  // (wave-uniform SGPRs: a per-piece select spilled them to scratch)
+  constexpr int NPP = MID / PROWS;
+  static_assert(NPP % PPW == 0 && PPW * NW == 2 * NPP, "W ring piece map");
+  const bool bq = wave * PPW / NPP != 0;
   const __amdgpu_buffer_rsrc_t wq0 = bq ? wr[0][1] : wr[0][0], wq1 = bq ? wr[1][1] : wr[1][0];
   int bnrow[PPW], bch[PPW], bdst[PPW];
 #pragma unroll
   for (int i = 0; i < PPW; ++i) {
     const int j = wave * PPW + i;
-    bnrow[i] = (j % NJ1) * 16 + (lane >> 2);
+    bnrow[i] = (j % NPP) * PROWS + ((lane >> 2) & (PROWS - 1));
     bch[i] = (lane & 3) ^ swzF(bnrow[i]);
-    bdst[i] = RING_OFF + ((j / NJ1) * MID + (j % NJ1) * 16) * 64;
+    bdst[i] = RING_OFF + ((j / NPP) * MID + (j % NPP) * PROWS) * 64;
   }
   auto issue_w = [&](int l, int kt, int stage) {           // l = 0 (W1) or 1 (W2)
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const unsigned vo = (unsigned)((bnrow[i] * p.kp[l] + bch[i] * 8) * 2);
-      bl_lds16(l ? wq1 : wq0, lds + bdst[i] + stage * STAGE, vo, kt * BK_ * 2);
+      if constexpr (S::HALF) {
+        if (lane < 32) bl_lds16(l ? wq1 : wq0, lds + bdst[i] + stage * STAGE, vo, kt * BK_ * 2);
+      } else {
+        bl_lds16(l ? wq1 : wq0, lds + bdst[i] + stage * STAGE, vo, kt * BK_ * 2);
+      }
     }
   };
   // the W stream: steps u < NK1 are W1's K-steps, the next 18 W2's; step u goes to stage u % RING
@@ -390,8 +410,8 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void b
     unsigned char* const w3b = lds + W3_OFF + (W3DB ? (h & 1) * W3_PART : 0);
     constexpr int RB3 = R3 / 16;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = wave * 4 + i;
+    for (int i = 0; i < PW3; ++i) {
+      const int idx = wave * PW3 + i;
       const int rb = idx % RB3, q = (idx / RB3) & 1, ks = idx / (2 * RB3);
       const int nrow = rb * 16 + (lane >> 2);
       const int ch = (lane & 3) ^ swzF(nrow);
@@ -521,17 +541,38 @@ __global__ __launch_bounds__(NW * 64, (BShape<MIDT, PROJ>::WPC * NW / 4)) void b
 
 }  // namespace
 
-int bneck_launch(const BneckK& kp0, hipStream_t st) {
-  BneckK kp = kp0;
+// tile rows: 8 (one workgroup of 8 waves per 8 x 16 tile, two per CU at inner width 64).
+// PRPE_BNECK_TR=16 selects the 16 x 16-pixel, 16-wave tile for the inner-width-64 blocks (A/B
+// runs, round 5): it halves the weight bytes staged per pixel and the halo (1.41x -> 1.27x) but
+// measured slower -- layer1 identity block 5.21 -> 5.80 ms, projection 4.05 -> 4.38 ms at bs = 256
+// (profiles/r05_bneck_ablate.txt): one 16-wave workgroup per CU stalls every wave at each
+// barrier where two 8-wave workgroups cover each other's, and phase 1's 21 haloed row blocks
+// leave 11 of 16 waves idle for half the phase
+int bneck_rows(int mid) {
+  static const int tr = [] {
+    const char* e = getenv("PRPE_BNECK_TR");
+    return e && e[0] == '1' && e[1] == '6' ? 16 : 8;
+  }();
+  return mid == 64 ? tr : 8;
+}
+
+template <int MIDT, bool PROJ, int TRT>
+int bneck_launch_t(BneckK kp, hipStream_t st) {
   kp.tiles_w = (kp.W + TC - 1) / TC;
-  kp.tiles_h = (kp.H + TR - 1) / TR;
+  kp.tiles_h = (kp.H + TRT - 1) / TRT;
   const int64_t nwg = (int64_t)kp.N * kp.tiles_w * kp.tiles_h;
   if (nwg <= 0 || nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
-  if (kp.proj) hipLaunchKernelGGL((bneck_kernel<64, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
-  else if (kp.mid == 64) hipLaunchKernelGGL((bneck_kernel<64, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
-  else hipLaunchKernelGGL((bneck_kernel<128, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  hipLaunchKernelGGL((bneck_kernel<MIDT, PROJ, TRT>), dim3(kp.nwg), dim3(TRT * 64), 0, st, kp);
   return launch_status();
+}
+
+int bneck_launch(const BneckK& kp, int rows, hipStream_t st) {
+  if (rows == 16 && kp.mid == 64)
+    return kp.proj ? bneck_launch_t<64, true, 16>(kp, st) : bneck_launch_t<64, false, 16>(kp, st);
+  if (rows != 8) return PRPE_EINVAL;
+  if (kp.proj) return bneck_launch_t<64, true, 8>(kp, st);
+  return kp.mid == 64 ? bneck_launch_t<64, false, 8>(kp, st) : bneck_launch_t<128, false, 8>(kp, st);
 }
 
 }  // namespace prpe_k
@@ -569,5 +610,5 @@ extern "C" int prpe_bottleneck(const prpe_bneck_desc* d, void* stream) {
     kp.wh[l] = d->w_h16[l]; kp.wl[l] = d->w_l16[l]; kp.kp[l] = d->k_pad[l];
     kp.sc[l] = d->scale16[l]; kp.bi[l] = d->bias[l];
   }
-  return bneck_launch(kp, as_stream(stream));
+  return bneck_launch(kp, bneck_rows(MID), as_stream(stream));
 }

@@ -37,7 +37,12 @@ constexpr int GBK = 32;
 // F16: precision 3 (fp16 planes of the per-frame-scaled activations, the weights' fp16 planes
 // pre-scaled per output channel; the per-row inverse scale in the epilogue), as conv_wave.hip.
 // BM = 128 (tile 43): 128 x 128 at 2 stages = 64 KB of LDS, two workgroups (16 waves) per CU
-template <int BN, int WM, int STAGES, bool APL, bool F16, int BM = 256>
+// PRIO (A/B, round 5; cdna_hip_programming.md T5): 1 = s_setprio(1) around each row block's MFMA
+// cluster, 2 = the static form (the second-dispatched half, waves 4-7, at priority 1 for the whole
+// K-loop), 0 = none
+// EARLY (A/B, round 5): every DMA piece of the step issued right after the barrier (the
+// minimum-2-phase recipe, cdna_hip_programming.md T3+T4) instead of one per row block.
+template <int BN, int WM, int STAGES, bool APL, bool F16, int BM = 256, int PRIO = 0, bool EARLY = false>
 __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK p) {
   static_assert(!(APL && F16), "planes input is precision 0");
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
@@ -115,6 +120,8 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
     for (int i = 0; i < PW; ++i) piece(i, nk > 1 ? 1 : 0, 1);
   }
 
+  if constexpr (PRIO == 2)
+    if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
   int st = 0;
   for (int kt = 0; kt < nk; ++kt) {
     // step kt landed (with 3 stages the PW pieces of step kt+1 may stay in flight)
@@ -126,6 +133,12 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
     const bool more = STAGES == 3 || kt + 1 < nk;
     const unsigned char* sa = lds + st * STAGE;
     const unsigned char* sb = sa + A_BYTES;
+    if constexpr (EARLY) {
+      if (more) {
+#pragma unroll
+        for (int u = 0; u < PW; ++u) piece(u, ks, sn);
+      }
+    }
     // B fragments of the wave's 4 column blocks (both planes), held for the whole step
     frag_t bfr[TN][NP];
 #pragma unroll
@@ -137,7 +150,7 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
     }
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      if (more) {                                       // the DMA pieces spread over the row blocks
+      if (!EARLY && more) {                             // the DMA pieces spread over the row blocks
 #pragma unroll
         for (int u = PW * i / TM; u < PW * (i + 1) / TM; ++u) piece(u, ks, sn);
       }
@@ -167,16 +180,19 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
         for (int q = 0; q < NP; ++q)
           af[q] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
       }
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int s = NP - 1; s >= 0; --s)
 #pragma unroll
           for (int qa = s; qa >= 0; --qa) acc[i][j] = mfma16(af[qa], bfr[j][s - qa], acc[i][j]);
+      if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
     }
     st = st + 1 == STAGES ? 0 : st + 1;
   }
   wait_barrier<0>();
+  if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
 
   // ---------------- epilogue: per-wave 16-row x 64-column slices, 16-B row stores
   float* ct = reinterpret_cast<float*>(lds) + wave * 16 * CS;
@@ -251,7 +267,7 @@ bool conv_gemm_eligible(const ConvK& kp, int prec) {
          !kp.in_scale && !kp.x2 && kp.xsw % 4 == 0;
 }
 
-template <int BN, int WM, int STAGES, int BM = 256>
+template <int BN, int WM, int STAGES, int BM = 256, int PRIO = 0, bool EARLY = false>
 int launch_gemm(const ConvK& kp0, int prec, hipStream_t st) {
   if (kp0.Co % BN) return PRPE_EINVAL;
   ConvK kp = kp0;
@@ -260,19 +276,25 @@ int launch_gemm(const ConvK& kp0, int prec, hipStream_t st) {
   if (nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
   const dim3 g(kp.nwg), b(512);
-  if (prec == 3) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, true, BM>), g, b, 0, st, kp);
-  else if (kp.x_planes) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, true, false, BM>), g, b, 0, st, kp);
-  else hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, false, BM>), g, b, 0, st, kp);
+  if (prec == 3) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, true, BM, PRIO, EARLY>), g, b, 0, st, kp);
+  else if (kp.x_planes) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, true, false, BM, PRIO, EARLY>), g, b, 0, st, kp);
+  else hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, false, BM, PRIO, EARLY>), g, b, 0, st, kp);
   return launch_status();
 }
 
 // tile 40 = auto (256 x 128, 3 stages), 41 = 256 x 256 (2 stages), 42 = 256 x 128 (2 stages),
-// 43 = 128 x 128 (2 stages, two workgroups per CU)
+// 43 = 128 x 128 (2 stages, two workgroups per CU); 44 / 45 = tile 40 with PRIO 1 / 2, 46 = tile
+// 41 with PRIO 1, 47 / 48 = tiles 41 / 40 with PRIO 1 and EARLY (A/B)
 int conv_gemm_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
   switch (tile) {
     case 41: return launch_gemm<256, 2, 2>(kp, prec, st);
     case 42: return launch_gemm<128, 4, 2>(kp, prec, st);
     case 43: return launch_gemm<128, 4, 2, 128>(kp, prec, st);
+    case 44: return launch_gemm<128, 4, 3, 256, 1>(kp, prec, st);
+    case 45: return launch_gemm<128, 4, 3, 256, 2>(kp, prec, st);
+    case 46: return launch_gemm<256, 2, 2, 256, 1>(kp, prec, st);
+    case 47: return launch_gemm<256, 2, 2, 256, 1, true>(kp, prec, st);
+    case 48: return launch_gemm<128, 4, 3, 256, 1, true>(kp, prec, st);
     default: return launch_gemm<128, 4, 3>(kp, prec, st);
   }
 }

@@ -760,11 +760,11 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const char* e = getenv("PRPE_CONV_GEMM_P3");
     return e && e[0] == '1' ? 1 : 0;
   }();
-  // PRPE_GEMM_TILE=41|42|43 overrides the automatic GEMM tile (A/B runs)
+  // PRPE_GEMM_TILE=41..48 overrides the automatic GEMM tile (A/B runs)
   static const int gemm_tile = [] {
     const char* e = getenv("PRPE_GEMM_TILE");
     const int t = e ? atoi(e) : 40;
-    return t == 41 || t == 42 || t == 43 ? t : 40;
+    return t >= 41 && t <= 48 ? t : 40;
   }();
   // PRPE_GEMM_MIN_KN=<n> keeps GEMMs with K * Co below n on the wave kernel (A/B runs)
   static const int64_t gemm_min_kn = [] {

@@ -12,6 +12,13 @@ on each in turn). Measurement only: none of these ship.
      the same
   D  A + s_waitcnt vmcnt(0) after each part's y stores (before the next part's residual loads):
      the W3 pieces land before the residual loads are issued, the stores are drained too
+  (round 5, second batch -- A-D all failed identically, so not an ordering race; what fails is
+   exactly the kernels whose phase-1 tile-max slots (wmax1, ring stage (NK1 - 1) % 4) sit at the
+   SB3 address: identity mid 64 (NK1 = 8) and mid 128 (NK1 = 16) use stage 3, the passing
+   projection block (NK1 = 2) stage 1)
+  E  A with SB3 at ring stage 2 + 1 KiB (past the phase-3 tile-max slots; no phase-1 access there)
+  F  A with the phase-1 tile-max slots moved to ring stage 2 + 4 KiB (away from SB3)
+  G  A with SB3 filled by register staging (global loads + ds_write) instead of LDS-DMA
 """
 import glob
 import os
@@ -38,6 +45,17 @@ def variants(src):
     st = "      bs_f4(yr, v, yvo, (h * R3 + j * 16) * 4);\n    }\n"
     assert src.count(st) == 1
     out["D"] = src.replace(st, st + '    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");\n')
+    sb = "  constexpr int SB3_OFF = RING_OFF + 3 * STAGE;"
+    assert sb in src
+    out["E"] = src.replace(sb, "  constexpr int SB3_OFF = RING_OFF + 2 * STAGE + 1024;")
+    wm = "reinterpret_cast<float*>(lds + RING_OFF + ((NK1 - 1) % RING) * STAGE);"
+    assert wm in src
+    out["F"] = src.replace(wm, "reinterpret_cast<float*>(lds + RING_OFF + 2 * STAGE + 4096);")
+    dma = """      bl_lds16(buf_rsrc(arr ? p.bi[2] : p.sc[2], CIO * 4), lds + SB3_OFF + (arr * CIO + pc * 256) * 4,
+               (unsigned)(pc * 1024 + lane * 16), 0);"""
+    assert dma in src, "dma"
+    out["G"] = src.replace(dma, """      const float* srcp = (arr ? p.bi[2] : p.sc[2]) + pc * 256 + lane * 4;
+      *reinterpret_cast<f4*>(lds + SB3_OFF + (arr * CIO + pc * 256) * 4 + lane * 16) = *reinterpret_cast<const f4*>(srcp);""")
     return out
 
 
