@@ -126,6 +126,16 @@ __device__ __forceinline__ void bs_f4(__amdgpu_buffer_rsrc_t r, f4 v, unsigned v
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u, v), r, voff, soff, 0);
 }
 
+// gfx950 store-data hazard: a 128-bit buffer store reads its data VGPRs after
+// it issues, and a VALU / MFMA write of them in the very next instruction replaces the data
+// (round 4's reverted 8308d2f wrote garbage so). LLVM's hazard model exempts stores whose soffset
+// is an SGPR, so nothing stops the scheduler from emitting that; this keeps v's registers live
+// through an `s_nop 1` ordered after the store (a side-effecting asm stays behind the store), two
+// wait states before any reuse. tools/barrier_hoist_check.py check 3 guards every kernel.
+__device__ __forceinline__ void store_data_guard(f4 v) {
+  asm volatile("s_nop 1" ::"v"(__builtin_bit_cast(v4u, v)));
+}
+
 // B fragments of column block j from a [2 planes][rows][64 B] stage (conv_wave's slot swizzle)
 __device__ __forceinline__ void b_frags(const unsigned char* sb, int rows, int j, int fr, int fg, f16x8 (&b)[2]) {
   const int nrow = j * 16 + fr;
@@ -421,6 +431,21 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
   };
   // (fence: the x loads above and the W3 pieces stay in separate scheduling regions, so no
   // counted wait's window can depend on their relative order; tools/barrier_hoist_check.py)
+  // conv3's scale / bias (CIO floats each) into ring stage 3 (free since the barrier above) by
+  // LDS-DMA, older than every phase-3 access the counted waits below count: the epilogue reads
+  // them from LDS. Loaded into registers there, they were the youngest vector-memory ops at each
+  // use, so the compiler's wait for them (vmcnt(0), one in-order counter) also drained the part's
+  // previous y stores: store -> load -> wait -> store, serialised per 16 columns.
+  constexpr int SB3_OFF = RING_OFF + 3 * STAGE;
+  static_assert(2 * CIO * 4 <= STAGE && 2 * (CIO / 256) <= NW, "SB3: one 1-KiB piece per wave");
+  {
+    constexpr int NSB = CIO / 256;                           // 1-KiB pieces per array
+    if (wave < 2 * NSB) {
+      const int arr = wave / NSB, pc = wave % NSB;
+      bl_lds16(buf_rsrc(arr ? p.bi[2] : p.sc[2], CIO * 4), lds + SB3_OFF + (arr * CIO + pc * 256) * 4,
+               (unsigned)(pc * 1024 + lane * 16), 0);
+    }
+  }
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   issue_w3(0);
@@ -521,7 +546,8 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c0 = h * R3 + j * 16 + fg * 4;
-      const f4 s = *reinterpret_cast<const f4*>(p.sc[2] + c0), b = *reinterpret_cast<const f4*>(p.bi[2] + c0);
+      const float* const sb3 = reinterpret_cast<const float*>(lds + SB3_OFF);
+      const f4 s = *reinterpret_cast<const f4*>(sb3 + c0), b = *reinterpret_cast<const f4*>(sb3 + CIO + c0);
       f4 v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -531,6 +557,7 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
         ymax = fmaxf(ymax, v[r]);
       }
       bs_f4(yr, v, yvo, (h * R3 + j * 16) * 4);
+      store_data_guard(v);
     }
     asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);             // (the counted waits assume this issue order)

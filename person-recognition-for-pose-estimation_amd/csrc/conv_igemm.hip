@@ -771,9 +771,20 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const char* e = getenv("PRPE_GEMM_MIN_KN");
     return e ? (int64_t)atoll(e) : (int64_t)0;
   }();
+  // the 256 x 256 tile (41) for the GEMMs that write the planes format through an activation
+  // (ViT fc1: GELU, face-YOLO adapter.7: SiLU), the 256 x 128 one (40) for the rest: measured in
+  // the model at bs = 256 (profiles/r05_layer_profile_gemm_tiles.txt): fc1 0.783 -> 0.725 ms,
+  // adapter.7 6.71 -> 6.33 ms on 41, while fc2 / proj (residual epilogues) and qkv lose on it
+  // (0.636 -> 0.729, 0.220 -> 0.264, 0.526 -> 0.542). PRPE_GEMM_WIDE=0 keeps 40 everywhere (A/B).
+  static const int gemm_wide = [] {
+    const char* e = getenv("PRPE_GEMM_WIDE");
+    return e && e[0] == '0' ? 0 : 1;
+  }();
   if (tile == 0 && gemm_on && (kp.x_planes || (prec == 3 && gemm_p3)) && kp.M >= (1 << 15) &&
-      (int64_t)kp.K * kp.Co >= gemm_min_kn && conv_gemm_eligible(kp, prec))
-    return conv_gemm_launch(kp, prec, gemm_tile, st);
+      (int64_t)kp.K * kp.Co >= gemm_min_kn && conv_gemm_eligible(kp, prec)) {
+    const bool wide = gemm_wide && gemm_tile == 40 && kp.y_planes && kp.act != PRPE_ACT_NONE && kp.Co % 256 == 0;
+    return conv_gemm_launch(kp, prec, wide ? 41 : gemm_tile, st);
+  }
   if (tile >= 30 && tile < 40)
     return conv_halo_eligible(kp, prec, km, tile) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;
   if (tile == 0 && halo_on && conv_halo_auto(kp, prec) && conv_halo_eligible(kp, prec, km))

@@ -26,6 +26,14 @@ on the control-flow graph of every kernel (loop back-edges included):
    LDS through M0 at an address the compiler cannot separate from the others'. Ops the compiler
    ADDS -- scratch spills -- only make a count more conservative: a perf lint, below.)
 
+3. Store data overwritten too early (round 5): a buffer / global store of more
+   than 64 bits whose data VGPRs a VALU or MFMA writes within ``STORE_DATA_STATES`` wait states
+   after it, on some CFG path. LLVM's hazard recognizer skips this for buffer stores with an SGPR
+   soffset; on gfx950 it corrupts the stored data (the reverted commit 8308d2f: nine such stores,
+   layer1 garbage; the same stream with ``s_nop 1`` after each store passed, with it before each
+   store failed, tools/bneck_8308_nop.py). The source-level fix is conv_bneck.hip's
+   ``store_data_guard``.
+
 Perf lints (``--lint``, informational): compiler waits that drain a just-issued store (a load
 issued behind a store: the round-3 bottleneck epilogue), and scratch accesses in kernels with
 counted waits.
@@ -45,6 +53,7 @@ BRANCH = re.compile(r"^s_(c)?branch\w*\s+(\.LBB\w+)")
 STORE_PREFIX = ("ds_write", "ds_store", "buffer_store", "global_store", "scratch_store", "flat_store")
 VMEM_PREFIX = ("buffer_", "global_", "scratch_", "flat_", "tbuffer_")
 VMEM_NOT_COUNTED = ("buffer_inv", "buffer_wbl2", "buffer_wbinvl1", "buffer_gl")
+STORE_DATA_STATES = 1                  # wait states a >64-bit store's data VGPRs must stay unwritten
 
 
 def regs(txt):
@@ -277,6 +286,48 @@ class Kernel:
         return waits, nwin, viol
 
 
+    # ---- check 3: store data overwritten inside the store's data-read window
+    def store_data_overwrites(self, states=STORE_DATA_STATES):
+        """A buffer / global store of more than 64 bits reads its data VGPRs some cycles after
+        it issues; a VALU write of those VGPRs fewer than ``states`` wait states later (an
+        ``s_nop N`` counts N + 1, any other instruction 1; followed along every CFG path) can
+        replace the data before it is read.  LLVM models this hazard only for stores whose
+        soffset is not an SGPR, so the compiler emits it freely for ``buffer_store ... sN offen``.
+        On gfx950 it is real: the reverted commit 8308d2f's identity-block epilogue had nine such
+        stores and wrote garbage; two wait states after each (tools/bneck_8308_nop.py) fixed it."""
+        out = []
+        for it in self.insts:
+            if not it.mn.startswith(("buffer_store_dwordx3", "buffer_store_dwordx4", "global_store_dwordx3",
+                                     "global_store_dwordx4", "flat_store_dwordx3", "flat_store_dwordx4")):
+                continue
+            ops = [o.strip() for o in it.ops.split(",")]
+            data = regs(ops[1] if it.mn.startswith(("global_", "flat_")) else ops[0])
+            stack, hit = [(it.block, it.idx + 1, 0)], None
+            seen = set()
+            while stack and hit is None:
+                bi, start, ws = stack.pop()
+                _, b = self.blocks[bi]
+                for i in range(start, b):
+                    if ws >= states:
+                        break
+                    x = self.insts[i]
+                    if x.text == "FENCE":
+                        continue
+                    if x.mn.startswith("v_") and data & x.writes():
+                        hit = x
+                        break
+                    m = re.match(r"s_nop\s+(\d+)", x.text)
+                    ws += int(m.group(1)) + 1 if m else 1
+                else:
+                    for s_ in self.succ[bi]:
+                        if (s_, ws) not in seen:
+                            seen.add((s_, ws))
+                            stack.append((s_, self.blocks[s_][0], ws))
+            if hit is not None:
+                out.append((it, hit))
+        return out
+
+
 def store_drains(k):
     """Perf lint: compiler-inserted ``s_waitcnt vmcnt(N)`` for a load issued right after a STORE
     (a store among the three youngest ops the wait must complete, on some path): one in-order
@@ -313,13 +364,20 @@ def compile_asm(src, out):
 
 
 def check_asm(path, verbose=False, label=None, lint=False):
-    """-> (hoisted ds_reads, order violations, counted waits, windows) summed over the kernels."""
+    """-> (hoisted ds_reads, order violations, counted waits, windows, store-data overwrites)
+    summed over the kernels."""
     lines = open(path).read().split("\n")
     label = label or os.path.basename(path)
-    nh = nv = nw = nwin = 0
+    nh = nv = nw = nwin = ns = 0
     for k in kernels_of(lines):
         h = k.hoisted_reads()
         waits, nwin_k, v = k.order_violations()
+        sd = k.store_data_overwrites()
+        ns += len(sd)
+        if sd:
+            print(f"{label} {k.name[:90]}: {len(sd)} store(s) whose data VGPRs the next instruction overwrites")
+            for st, x in sd[:4]:
+                print("    ", st.line, st.text, "|", x.text)
         nh += len(h)
         nv += len(v)
         nw += len(waits)
@@ -343,7 +401,7 @@ def check_asm(path, verbose=False, label=None, lint=False):
                       f"(asm lines {', '.join(str(x.line) for x in d[:6])})")
         if verbose and waits:
             print(f"{label} {k.name[:90]}: {len(waits)} counted wait(s), {nwin_k} issue-order window(s) checked")
-    return nh, nv, nw, nwin
+    return nh, nv, nw, nwin, ns
 
 
 def main():
@@ -352,7 +410,7 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--lint", action="store_true", help="also list compiler waits that drain a store")
     a = ap.parse_args()
-    tot = [0, 0, 0, 0]
+    tot = [0, 0, 0, 0, 0]
     for src in a.srcs:
         with tempfile.TemporaryDirectory() as td:
             out = os.path.join(td, "k.s")
@@ -365,7 +423,8 @@ def main():
     print(f"counted vmcnt waits: {tot[2]}, issue-order windows checked: {tot[3]}")
     print("total hoisted ds_reads:", tot[0])
     print("total issue-order violations:", tot[1])
-    return 1 if tot[0] or tot[1] else 0
+    print("total store-data overwrites:", tot[4])
+    return 1 if tot[0] or tot[1] or tot[4] else 0
 
 
 if __name__ == "__main__":

@@ -19,6 +19,11 @@ on each in turn). Measurement only: none of these ship.
   E  A with SB3 at ring stage 2 + 1 KiB (past the phase-3 tile-max slots; no phase-1 access there)
   F  A with the phase-1 tile-max slots moved to ring stage 2 + 4 KiB (away from SB3)
   G  A with SB3 filled by register staging (global loads + ds_write) instead of LDS-DMA
+  (third batch -- E and G failed exactly as A, F worse: neither the copy mechanism nor its place)
+  J  A with the epilogue reading scale / bias from global memory again (the SB3 copy still made,
+     unused): does the copy corrupt anything, or is it the epilogue's LDS read?
+  K  A with the epilogue's bias from global memory, the scale from LDS
+  L  A with the epilogue's scale from global memory, the bias from LDS
 """
 import glob
 import os
@@ -56,6 +61,14 @@ def variants(src):
     assert dma in src, "dma"
     out["G"] = src.replace(dma, """      const float* srcp = (arr ? p.bi[2] : p.sc[2]) + pc * 256 + lane * 4;
       *reinterpret_cast<f4*>(lds + SB3_OFF + (arr * CIO + pc * 256) * 4 + lane * 16) = *reinterpret_cast<const f4*>(srcp);""")
+    rd = """      const float* const sb3 = reinterpret_cast<const float*>(lds + SB3_OFF);
+      const f4 s = *reinterpret_cast<const f4*>(sb3 + c0), b = *reinterpret_cast<const f4*>(sb3 + CIO + c0);"""
+    assert rd in src, "rd"
+    out["J"] = src.replace(rd, """      const f4 s = *reinterpret_cast<const f4*>(p.sc[2] + c0), b = *reinterpret_cast<const f4*>(p.bi[2] + c0);""")
+    out["K"] = src.replace(rd, """      const float* const sb3 = reinterpret_cast<const float*>(lds + SB3_OFF);
+      const f4 s = *reinterpret_cast<const f4*>(sb3 + c0), b = *reinterpret_cast<const f4*>(p.bi[2] + c0);""")
+    out["L"] = src.replace(rd, """      const float* const sb3 = reinterpret_cast<const float*>(lds + SB3_OFF);
+      const f4 s = *reinterpret_cast<const f4*>(p.sc[2] + c0), b = *reinterpret_cast<const f4*>(sb3 + CIO + c0);""")
     return out
 
 

@@ -3,7 +3,7 @@ design) for tools/bneck_ablate.sh: each variant is a scratch copy of csrc/conv_b
 parts of the kernel compiled out, compiled to an object and linked with the current build's
 other objects and its build_info.o (same source hash, so prpe._lib loads it on the box).
 
-    python tools/bneck_ablate_build.py            # -> tools/abl/libprpe_abl{1..7}.so
+    python tools/bneck_ablate_build.py [K ...]    # -> tools/abl/libprpe_ablK.so (default 4 5 6 7)
 
 variants (round 4 had 1-4; round 5 adds 5-7 for the weight stream):
   1  phase-2 (3x3) MFMAs out          2  phase-1 MFMAs out        3  phase-3 MFMAs out
@@ -61,7 +61,9 @@ def main():
     others = [o for o in glob.glob(os.path.join(BUILD, "*.o")) if not o.endswith("conv_bneck.o")]
     assert any(o.endswith("build_info.o") for o in others), "run build.py first"
     src0 = open(os.path.join(CSRC, "conv_bneck.hip")).read()
-    for k, (phases, wdma, xload) in VARIANTS.items():
+    want = [int(v) for v in sys.argv[1:]] or [4, 5, 6, 7]
+    for k in want:
+        phases, wdma, xload = VARIANTS[k]
         s = patch(src0, phases, wdma, xload)
         tmp = os.path.join(OUT, f"conv_bneck_abl{k}.hip")
         open(tmp, "w").write(s)
@@ -74,6 +76,7 @@ def main():
                            capture_output=True, text=True)
         if r.returncode:
             sys.exit(f"link {k}: {r.stderr[-2000:]}")
+        os.remove(obj)
         print("built", os.path.relpath(lib, ROOT), flush=True)
 
 

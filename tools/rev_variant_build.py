@@ -1,0 +1,44 @@
+"""Build an A/B library (container; measurement only): one csrc file taken from a git revision,
+linked with the current build's other objects and its build_info.o (same source hash, so
+prpe._lib loads it on the box in place of libprpe.so; tools/bneck_ablate.sh-style swap).
+
+    python tools/rev_variant_build.py REV csrc/conv_bneck.hip TAG   # -> tools/abl/libprpe_TAG.so
+
+Run after person-recognition-for-pose-estimation_amd/build.py (it reuses build/*.o).
+"""
+import glob
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "person-recognition-for-pose-estimation_amd")
+BUILD = os.path.join(PKG, "build")
+OUT = os.path.join(ROOT, "tools", "abl")
+HIPCC = "/opt/rocm/bin/hipcc"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I" + os.path.join(ROOT, "include"),
+         "-I" + os.path.join(PKG, "csrc"), "-Wno-unused-result"]
+
+
+def main():
+    rev, rel, tag = sys.argv[1:4]
+    name = os.path.basename(rel)
+    os.makedirs(OUT, exist_ok=True)
+    src = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:person-recognition-for-pose-estimation_amd/{rel}"],
+                         capture_output=True, text=True, check=True).stdout
+    stem = name.rsplit(".", 1)[0]
+    others = [o for o in glob.glob(os.path.join(BUILD, "*.o")) if os.path.basename(o) != stem + ".o"]
+    assert any(o.endswith("build_info.o") for o in others), "run build.py first"
+    tmp = os.path.join(OUT, f"{stem}_{tag}.hip")
+    open(tmp, "w").write(src)
+    obj = tmp[:-4] + ".o"
+    subprocess.run([HIPCC, *FLAGS, "-c", tmp, "-o", obj], check=True)
+    lib = os.path.join(OUT, f"libprpe_{tag}.so")
+    subprocess.run([HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", *others, obj, "-o", lib], check=True)
+    os.remove(obj)
+    os.remove(tmp)
+    print("built", os.path.relpath(lib, ROOT))
+
+
+if __name__ == "__main__":
+    main()
