@@ -3,6 +3,8 @@ linked with the current build's other objects and its build_info.o (same source 
 prpe._lib loads it on the box in place of libprpe.so; tools/bneck_ablate.sh-style swap).
 
     python tools/rev_variant_build.py REV csrc/conv_bneck.hip TAG   # -> tools/abl/libprpe_TAG.so
+    python tools/rev_variant_build.py WORK csrc/conv_halo.hip TAG --patch OLD NEW [--patch ...]
+        (WORK = the working tree's file; each OLD must occur in it; measurement variants)
 
 Run after person-recognition-for-pose-estimation_amd/build.py (it reuses build/*.o).
 """
@@ -22,10 +24,20 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I" + os.path.j
 
 def main():
     rev, rel, tag = sys.argv[1:4]
+    rest = sys.argv[4:]
     name = os.path.basename(rel)
     os.makedirs(OUT, exist_ok=True)
-    src = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:person-recognition-for-pose-estimation_amd/{rel}"],
-                         capture_output=True, text=True, check=True).stdout
+    if rev == "WORK":
+        src = open(os.path.join(PKG, rel)).read()
+    else:
+        src = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:person-recognition-for-pose-estimation_amd/{rel}"],
+                             capture_output=True, text=True, check=True).stdout
+    while rest:
+        assert rest[0] == "--patch" and len(rest) >= 3, "usage: --patch OLD NEW"
+        old, new = rest[1], rest[2]
+        assert old in src, f"not found: {old}"
+        src = src.replace(old, new)
+        rest = rest[3:]
     stem = name.rsplit(".", 1)[0]
     others = [o for o in glob.glob(os.path.join(BUILD, "*.o")) if os.path.basename(o) != stem + ".o"]
     assert any(o.endswith("build_info.o") for o in others), "run build.py first"
