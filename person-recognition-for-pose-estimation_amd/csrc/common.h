@@ -265,6 +265,11 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base, int
 __device__ __forceinline__ void bl_lds16(__amdgpu_buffer_rsrc_t r, void* dst_lds, unsigned voff, int soff) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst_lds), 16, voff, soff, 0, 0);
 }
+// the same with the non-temporal policy (cache-policy bit nt): for input streamed once per tile,
+// so L2 evicts it first and keeps the weight planes every workgroup re-reads (conv_halo.hip)
+__device__ __forceinline__ void bl_lds16_nt(__amdgpu_buffer_rsrc_t r, void* dst_lds, unsigned voff, int soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)(dst_lds), 16, voff, soff, 0, 2);
+}
 constexpr unsigned BL_OOB = 0x80000000u;   // a voffset past every descriptor's range (num_records < 2^31)
 
 __device__ __forceinline__ int swzF(int row) { return (0x78 >> (((row >> 2) & 3) * 2)) & 3; }

@@ -756,10 +756,17 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     return e && e[0] == '0' ? 0 : 1;
   }();
   if (tile >= 40 && tile < 50) return conv_gemm_eligible(kp, prec) ? conv_gemm_launch(kp, prec, tile, st) : PRPE_EINVAL;
+  // precision 3 (the trunk's fp32 activations, split per frame) on the GEMM kernel: for the deep
+  // 1x1s without a residual (K >= 1024: layer3 / layer4 conv1, the heads' 2048-deep adapter .0),
+  // where it measured 10-13 % faster than the wave kernel's 256x128 tile in the model; the
+  // short-K residual conv3s (K = 256: +13 % on the GEMM) stay on the wave kernel
+  // (profiles/r05_layer_profile_p3gemm.txt). PRPE_CONV_GEMM_P3=1 routes every eligible
+  // precision-3 conv, =0 none (A/B runs).
   static const int gemm_p3 = [] {
     const char* e = getenv("PRPE_CONV_GEMM_P3");
-    return e && e[0] == '1' ? 1 : 0;
+    return e && e[0] == '1' ? 1 : e && e[0] == '0' ? 0 : 2;
   }();
+  const bool p3_gemm = prec == 3 && (gemm_p3 == 1 || (gemm_p3 == 2 && kp.K >= 1024 && kp.res_mode == PRPE_RES_NONE));
   // PRPE_GEMM_TILE=41..48 overrides the automatic GEMM tile (A/B runs)
   static const int gemm_tile = [] {
     const char* e = getenv("PRPE_GEMM_TILE");
@@ -780,7 +787,7 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const char* e = getenv("PRPE_GEMM_WIDE");
     return e && e[0] == '0' ? 0 : 1;
   }();
-  if (tile == 0 && gemm_on && (kp.x_planes || (prec == 3 && gemm_p3)) && kp.M >= (1 << 15) &&
+  if (tile == 0 && gemm_on && (kp.x_planes || p3_gemm) && kp.M >= (1 << 15) &&
       (int64_t)kp.K * kp.Co >= gemm_min_kn && conv_gemm_eligible(kp, prec)) {
     const bool wide = gemm_wide && gemm_tile == 40 && kp.y_planes && kp.act != PRPE_ACT_NONE && kp.Co % 256 == 0;
     return conv_gemm_launch(kp, prec, wide ? 41 : gemm_tile, st);

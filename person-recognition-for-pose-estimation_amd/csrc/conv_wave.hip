@@ -56,9 +56,20 @@ constexpr int BK = 32;
 // dominate, so one iteration covers TWO K-steps (KS = 2): the B stage holds the hi plane of
 // K-steps 2s and 2s+1 where the two-plane forms hold two planes of one step (same 16 KB at
 // BN = 128), and each accumulator takes step 2s then 2s+1 (the sequential order).
+// launch bound: HIP's second argument is waves per SIMD. The 8-wave 2-plane tiles of 32-row
+// waves without a prologue ask for 4 (two workgroups per CU, <= 128 VGPRs; they need 122-128):
+// the precision-3 256x128 tile (the trunk's unfused convs) sat at exactly 128 until the round-4/5
+// GELU rewrites grew the runtime-switched epilogue and it compiled to 132 -- one workgroup per CU,
+// those convs 15-27 % slower. The larger tiles keep 2 (their 150-240 VGPRs would
+// spill at 128). The precision-4 4-wave tile at two K-steps (KSF 1: AdaFace) likewise asks for
+// 4 waves per SIMD (four workgroups per CU at 128 VGPRs; it had grown to 132).
+template <int NW, int TM, int NP, bool PRO, bool ONE, int KSF>
+constexpr int wave_wps() {
+  return (NW == 8 && TM == 2 && NP == 2 && !PRO) || (NW == 4 && TM == 2 && ONE && KSF == 1 && !PRO) ? 4 : 2;
+}
 template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false,
           bool APL = false, bool ONE = false, int KSF = 0>
-__global__ __launch_bounds__(NW * 64, 2) void conv_wave_kernel(ConvK p) {
+__global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) void conv_wave_kernel(ConvK p) {
   static_assert(!APL || (NP == 2 && !F16 && !PRO && !DUAL), "planes input: two bf16 planes only");
   static_assert(!F16 || (NP == 2 && (!PRO || ONE)), "f16 planes: two planes, no prologue unless single-plane");
   static_assert(!ONE || (F16 && !DUAL && !APL), "single fp16 plane: precision 4");

@@ -177,3 +177,28 @@ def test_every_kernel_source_has_no_hoisted_reads_and_no_order_violations(asm_di
     assert len(asm_dir) >= 13
     assert waits >= 100 and windows >= waits          # the hand-counted waits were found and walked
     assert hoisted == 0 and viol == 0 and stores == 0, text
+
+
+def _kernel_meta(path):
+    """kernel name -> (VGPRs, VGPR spills) from the .s metadata."""
+    import re
+    out = {}
+    for blk in open(path).read().split("  - .agpr_count")[1:]:
+        name = re.search(r"\.name:\s+(\S+)", blk).group(1)
+        out[name] = (int(re.search(r"\.vgpr_count:\s+(\d+)", blk).group(1)),
+                     int(re.search(r"\.vgpr_spill_count:\s+(\d+)", blk).group(1)))
+    return out
+
+
+def test_occupancy_critical_tiles_fit_128_vgprs_without_spills(asm_dir):
+    # the precision-3 256x128 wave tile (the trunk's unfused convs) and the precision-4 4-wave
+    # two-K-step tile (AdaFace) run two / four workgroups per CU only at <= 128 VGPRs; round 5's
+    # GELU rewrite silently pushed them to 132 (one / three per CU: trunk convs 15-27 % slower).
+    # Their launch bound now asks for 4 waves per SIMD; this pins that it costs no spills.
+    meta = _kernel_meta([o for o in asm_dir if o.endswith("conv_wave.s")][0])
+    hot = {k: v for k, v in meta.items()
+           if "conv_wave_kernelILi8ELi2ELi8ELi2ELi3ELb0ELb1E" in k        # NW 8, TM 2, TN 8, p3, no prologue
+           or "conv_wave_kernelILi4ELi2ELi8ELi2ELi2ELb0ELb1ELb0ELb0ELb1ELi1E" in k}   # p4, KSF 1
+    assert len(hot) >= 3, sorted(meta)
+    for k, (v, spill) in hot.items():
+        assert v <= 128 and spill == 0, (k, v, spill)
