@@ -232,8 +232,7 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
       if constexpr (F16) v = v * ldexpf(1.f, f16_scale_exp(p.x_amax[mm[e] / p.HoWo]) - 15);
       v = v * sc4 + bi4;
       if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
+      v = apply_act4(v, p.act, sl4);   // packed GELU / SiLU, bit-identical to apply_act
       if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
       const int64_t yo = (int64_t)mm[e] * p.ysw + col;
       if (p.y_planes) {

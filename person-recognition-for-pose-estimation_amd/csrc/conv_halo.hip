@@ -403,8 +403,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
       if constexpr (F16) v = v * inv;
       v = v * sc4 + bi4;
       if (p.res_mode == PRPE_RES_PRE_ACT) v += res[e];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], p.act, sl4[q]);
+      v = apply_act4(v, p.act, sl4);   // packed GELU / SiLU, bit-identical to apply_act
       if (p.res_mode == PRPE_RES_POST_ACT) v += res[e];
       if constexpr (TAPS != 0) {                       // keep the activated value for the tap GEMM
         *reinterpret_cast<f4*>(ct + (rr0 + RPP * e) * CS + cc * 4) = v;
@@ -457,10 +456,11 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2))) vo
         __builtin_amdgcn_wave_barrier();
         if (wn == 0) {
 #pragma unroll
-          for (int jn = 0; jn < 4; ++jn)
+          for (int jn = 0; jn < 4; ++jn) {
+            const f32x4 t = apply_act4(zm[jn] * s2[jn] + b2[jn], p.act2, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
-            for (int r = 0; r < 4; ++r)
-              ct[(fg * 4 + r) * CS + jn * 16 + fr] = apply_act(zm[jn][r] * s2[jn] + b2[jn], p.act2, 0.f);
+            for (int r = 0; r < 4; ++r) ct[(fg * 4 + r) * CS + jn * 16 + fr] = t[r];
+          }
           __builtin_amdgcn_wave_barrier();
           slab_gemm<2, 64>(ct, CS, w3s, W3S, 32 * W3S, fr, fg, zc);
         }

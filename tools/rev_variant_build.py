@@ -4,7 +4,7 @@ prpe._lib loads it on the box in place of libprpe.so; tools/bneck_ablate.sh-styl
 
     python tools/rev_variant_build.py REV csrc/conv_bneck.hip TAG   # -> tools/abl/libprpe_TAG.so
     python tools/rev_variant_build.py WORK csrc/conv_halo.hip TAG --patch OLD NEW [--patch ...]
-        (WORK = the working tree's file; each OLD must occur in it; measurement variants)
+        (WORK = the working tree's file; measurement variants; csrc files may be comma-separated)
 
 Run after person-recognition-for-pose-estimation_amd/build.py (it reuses build/*.o).
 """
@@ -23,32 +23,39 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-I" + os.path.j
 
 
 def main():
-    rev, rel, tag = sys.argv[1:4]
+    rev, rels, tag = sys.argv[1:4]
     rest = sys.argv[4:]
-    name = os.path.basename(rel)
     os.makedirs(OUT, exist_ok=True)
-    if rev == "WORK":
-        src = open(os.path.join(PKG, rel)).read()
-    else:
-        src = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:person-recognition-for-pose-estimation_amd/{rel}"],
-                             capture_output=True, text=True, check=True).stdout
+    patches = []
     while rest:
         assert rest[0] == "--patch" and len(rest) >= 3, "usage: --patch OLD NEW"
-        old, new = rest[1], rest[2]
-        assert old in src, f"not found: {old}"
-        src = src.replace(old, new)
+        patches.append((rest[1], rest[2]))
         rest = rest[3:]
-    stem = name.rsplit(".", 1)[0]
-    others = [o for o in glob.glob(os.path.join(BUILD, "*.o")) if os.path.basename(o) != stem + ".o"]
+    objs, stems = [], []
+    for rel in rels.split(","):                 # several csrc files: comma-separated
+        name = os.path.basename(rel)
+        if rev == "WORK":
+            src = open(os.path.join(PKG, rel)).read()
+        else:
+            src = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:person-recognition-for-pose-estimation_amd/{rel}"],
+                                 capture_output=True, text=True, check=True).stdout
+        for old, new in patches:
+            if old in src:
+                src = src.replace(old, new)
+        stem = name.rsplit(".", 1)[0]
+        stems.append(stem)
+        tmp = os.path.join(OUT, f"{stem}_{tag}.hip")
+        open(tmp, "w").write(src)
+        obj = tmp[:-4] + ".o"
+        subprocess.run([HIPCC, *FLAGS, "-c", tmp, "-o", obj], check=True)
+        os.remove(tmp)
+        objs.append(obj)
+    others = [o for o in glob.glob(os.path.join(BUILD, "*.o")) if os.path.basename(o)[:-2] not in stems]
     assert any(o.endswith("build_info.o") for o in others), "run build.py first"
-    tmp = os.path.join(OUT, f"{stem}_{tag}.hip")
-    open(tmp, "w").write(src)
-    obj = tmp[:-4] + ".o"
-    subprocess.run([HIPCC, *FLAGS, "-c", tmp, "-o", obj], check=True)
     lib = os.path.join(OUT, f"libprpe_{tag}.so")
-    subprocess.run([HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", *others, obj, "-o", lib], check=True)
-    os.remove(obj)
-    os.remove(tmp)
+    subprocess.run([HIPCC, "-shared", "-fPIC", "--offload-arch=gfx950", *others, *objs, "-o", lib], check=True)
+    for o in objs:
+        os.remove(o)
     print("built", os.path.relpath(lib, ROOT))
 
 
