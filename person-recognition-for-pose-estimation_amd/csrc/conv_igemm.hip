@@ -756,15 +756,15 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     return e && e[0] == '0' ? 0 : 1;
   }();
   if (tile >= 40 && tile < 50) return conv_gemm_eligible(kp, prec) ? conv_gemm_launch(kp, prec, tile, st) : PRPE_EINVAL;
-  // precision 3 (the trunk's fp32 activations, split per frame) on the GEMM kernel: for the deep
-  // 1x1s without a residual (K >= 1024: layer3 / layer4 conv1, the heads' 2048-deep adapter .0),
-  // where it measured 10-13 % faster than the wave kernel's 256x128 tile in the model; the
-  // short-K residual conv3s (K = 256: +13 % on the GEMM) stay on the wave kernel
-  // (profiles/r05_layer_profile_p3gemm.txt). PRPE_CONV_GEMM_P3=1 routes every eligible
-  // precision-3 conv, =0 none (A/B runs).
+  // precision 3 (the trunk's fp32 activations, split per frame) on the GEMM kernel: off by
+  // default. PRPE_CONV_GEMM_P3=auto routes the deep 1x1s without a residual (K >= 1024), which
+  // measured 10-13 % faster than the wave kernel's 256x128 tile while that tile was held to one
+  // workgroup per CU by its 132-VGPR build (profiles/r05_layer_profile_p3gemm.txt); with the tile
+  // back at 128 VGPRs the wave kernel is the faster one again (profiles/r05_p3gemm_recheck.txt).
+  // =1 routes every eligible precision-3 conv (A/B runs).
   static const int gemm_p3 = [] {
     const char* e = getenv("PRPE_CONV_GEMM_P3");
-    return e && e[0] == '1' ? 1 : e && e[0] == '0' ? 0 : 2;
+    return e && e[0] == '1' ? 1 : e && e[0] == 'a' ? 2 : 0;
   }();
   const bool p3_gemm = prec == 3 && (gemm_p3 == 1 || (gemm_p3 == 2 && kp.K >= 1024 && kp.res_mode == PRPE_RES_NONE));
   // PRPE_GEMM_TILE=41..48 overrides the automatic GEMM tile (A/B runs)
