@@ -695,8 +695,14 @@ __global__ __launch_bounds__(NWAVE * 64) void vit_attention_h_kernel(const float
     bf16x8 qh[2], ql[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const float v[8] = {qr[2 * ks][0], qr[2 * ks][1], qr[2 * ks][2], qr[2 * ks][3],
-                          qr[2 * ks + 1][0], qr[2 * ks + 1][1], qr[2 * ks + 1][2], qr[2 * ks + 1][3]};
+      // q pre-scaled by scale * log2(e): the scores come out in base-2 units, so the softmax
+      // is v_exp_f32 of (s - max) directly (no per-score scale multiply, no two-part exp(x)
+      // argument: ~6 VALU per score less; the fp32 product adds 2^-24 relative to q, far below
+      // the 3-term bf16 split's own error)
+      const float qs = scale * 1.44269504088896340736f;
+      const float v[8] = {qr[2 * ks][0] * qs, qr[2 * ks][1] * qs, qr[2 * ks][2] * qs, qr[2 * ks][3] * qs,
+                          qr[2 * ks + 1][0] * qs, qr[2 * ks + 1][1] * qs, qr[2 * ks + 1][2] * qs,
+                          qr[2 * ks + 1][3] * qs};
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         __bf16 hi, lo;
@@ -711,7 +717,7 @@ __global__ __launch_bounds__(NWAVE * 64) void vit_attention_h_kernel(const float
     // two halves of 96 keys (register budget: 24 score registers per lane instead of 48), one
     // online-softmax merge between them: S^T tiles rows = keys 16 t + 4 fg + r, column = query
     // q0 + fr
-    float m = -1e30f, sum = 0.f;                         // finite: exp_hw(-inf) would be NaN
+    float m = -1e30f, sum = 0.f;                         // finite: (-inf) - (-inf) would be NaN
     f32x4 o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -739,17 +745,17 @@ __global__ __launch_bounds__(NWAVE * 64) void vit_attention_h_kernel(const float
 #pragma unroll
       for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { sc[t][r] *= scale; mx = fmaxf(mx, sc[t][r]); }
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sc[t][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mn = fmaxf(m, mx);
-      const float alpha = exp_hw(m - mn);                // 0 for the first half
+      const float alpha = __builtin_amdgcn_exp2f(m - mn); // 0 for the first half
       m = mn;
       float hs = 0.f;
 #pragma unroll
       for (int t = 0; t < HT; ++t)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) { const float e = exp_hw(sc[t][r] - mn); sc[t][r] = e; hs += e; }
+        for (int r = 0; r < 4; ++r) { const float e = __builtin_amdgcn_exp2f(sc[t][r] - mn); sc[t][r] = e; hs += e; }
       hs += __shfl_xor(hs, 16, 64);
       hs += __shfl_xor(hs, 32, 64);
       sum = sum * alpha + hs;
