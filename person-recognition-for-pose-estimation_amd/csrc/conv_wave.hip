@@ -415,8 +415,10 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
       if (ok[e]) {
         int64_t ro;
         offs(m, yo[e], ro);
-        // non-temporal residual loads and output stores (last use / not re-read here: the A panel
-        // re-read per column tile keeps its L2 lines), +0.35 % bench (profiles/r05_wave_nt_ab.txt)
+        // residual convs (the trunk's conv3s): non-temporal residual loads and output stores (last
+        // use / not re-read here: the A panel re-read per column tile keeps its L2 lines), +0.35 %
+        // bench; for the other convs NT stores cost the YOLO net ~1 % (its next layer re-reads
+        // the output from the caches), profiles/r05_nt_epilogue_ab.txt
         if (p.res_mode != PRPE_RES_NONE) res[e] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(p.r + ro));
         if (track) fn[e] = frame_of(m);
       }
@@ -446,7 +448,8 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
         *reinterpret_cast<bf16x4*>(y16) = pl[0];
         *reinterpret_cast<bf16x4*>(y16 + 8) = pl[1];
       } else {
-        __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p.y + yo[e]));
+        if (p.res_mode != PRPE_RES_NONE) __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p.y + yo[e]));
+        else *reinterpret_cast<f4*>(p.y + yo[e]) = v;
       }
       if (p.y_amax) {
         const float a = amax4(v);
