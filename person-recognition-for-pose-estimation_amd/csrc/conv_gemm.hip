@@ -42,7 +42,13 @@ constexpr int GBK = 32;
 // K-loop), 0 = none
 // EARLY (A/B, round 5): every DMA piece of the step issued right after the barrier (the
 // minimum-2-phase recipe, cdna_hip_programming.md T3+T4) instead of one per row block.
-template <int BN, int WM, int STAGES, bool APL, bool F16, int BM = 256, int PRIO = 0, bool EARLY = false>
+// PERSIST (round 5, tiles 49 / 47): a workgroup walks tiles t, t + G, ... (G = the grid, a few per
+// CU): right after a tile's last K-step its successor's first STAGES - 1 steps are DMA'd into the
+// ring while this tile's epilogue runs out of the last stage (its slab fits one stage), so the
+// ring refill and the workgroup launch no longer sit between two tiles' MFMAs. Same arithmetic
+// (bit-identical).
+template <int BN, int WM, int STAGES, bool APL, bool F16, int BM = 256, int PRIO = 0, bool EARLY = false,
+          bool PERSIST = false>
 __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK p) {
   static_assert(!(APL && F16), "planes input is precision 0");
   using frag_t = typename std::conditional<F16, f16x8, bf16x8>::type;
@@ -58,37 +64,44 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
   static_assert((NA + NBP) % NW == 0, "pieces");
   constexpr int CS = WTN + 4;                          // epilogue row pitch (floats)
   static_assert(NW * 16 * CS * 4 <= STAGES * STAGE, "epilogue slab");
+  static_assert(!PERSIST || NW * 16 * CS * 4 <= STAGE, "persistent: the slab fits the last stage");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[STAGES * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int fr = lane & 15, fg = lane >> 4;
   const int wm = wave / WN, wn = wave % WN;
-  const int L = xcd_remap(blockIdx.x, p.nwg);
-  const int tile_m = L / p.tiles_n, tile_n = L % p.tiles_n;
-  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  int t = blockIdx.x;                                  // tile index (PERSIST: t, t + G, ...)
+  int m0, n0;
 
   // ---- this wave's DMA pieces: j = wave * PW + i; j < NA: A rows 8j .. 8j+7, else B
   const float* src[PW];
   int dst[PW];
+  auto setup = [&](int tt) {
+    const int L = xcd_remap(tt, p.nwg);
+    const int tile_m = L / p.tiles_n, tile_n = L % p.tiles_n;
+    m0 = tile_m * BM;
+    n0 = tile_n * BN;
 #pragma unroll
-  for (int i = 0; i < PW; ++i) {
-    const int j = wave * PW + i;
-    if (j < NA) {
-      const int row = j * 8 + (lane >> 3);
-      const int s = (lane & 7) ^ swz_rows(row);            // logical slot landing in this lane's slot
-      const int m = m0 + row < p.M ? m0 + row : p.M - 1;   // tail rows re-read the last row
-      src[i] = p.x + (int64_t)m * p.xsw + s * 4;
-      dst[i] = j * 1024;
-    } else {
-      const int jb = j - NA;
-      const int q = jb / (BN / 16), rb = jb % (BN / 16);
-      const int nrow = rb * 16 + (lane >> 2);
-      const int ch = (lane & 3) ^ swzF(nrow);
-      const uint16_t* plane = F16 ? (q == 0 ? p.wh16 : p.wl16) : (q == 0 ? p.whi : p.wlo);
-      src[i] = reinterpret_cast<const float*>(plane + (int64_t)(n0 + nrow) * p.k_pad + ch * 8);
-      dst[i] = A_BYTES + (q * BN + rb * 16) * 64;
+    for (int i = 0; i < PW; ++i) {
+      const int j = wave * PW + i;
+      if (j < NA) {
+        const int row = j * 8 + (lane >> 3);
+        const int s = (lane & 7) ^ swz_rows(row);            // logical slot landing in this lane's slot
+        const int m = m0 + row < p.M ? m0 + row : p.M - 1;   // tail rows re-read the last row
+        src[i] = p.x + (int64_t)m * p.xsw + s * 4;
+        dst[i] = j * 1024;
+      } else {
+        const int jb = j - NA;
+        const int q = jb / (BN / 16), rb = jb % (BN / 16);
+        const int nrow = rb * 16 + (lane >> 2);
+        const int ch = (lane & 3) ^ swzF(nrow);
+        const uint16_t* plane = F16 ? (q == 0 ? p.wh16 : p.wl16) : (q == 0 ? p.whi : p.wlo);
+        src[i] = reinterpret_cast<const float*>(plane + (int64_t)(n0 + nrow) * p.k_pad + ch * 8);
+        dst[i] = A_BYTES + (q * BN + rb * 16) * 64;
+      }
     }
-  }
+  };
+  setup(t);
   // K-step advance of each piece's source: A 32 channels (floats), B 32 bf16 = 16 floats
   auto piece = [&](int i, int kt, int stage) {
     const int j = wave * PW + i;
@@ -96,6 +109,8 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
     glds16(s, lds + stage * STAGE + dst[i]);
   };
 
+  bool pre = false;                                    // PERSIST: this tile's first steps already issued
+  for (;;) {
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -113,11 +128,13 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
   }
 
   const int nk = p.nk;
+  if (!pre) {
 #pragma unroll
-  for (int i = 0; i < PW; ++i) piece(i, 0, 0);
-  if constexpr (STAGES == 3) {
+    for (int i = 0; i < PW; ++i) piece(i, 0, 0);
+    if constexpr (STAGES == 3) {
 #pragma unroll
-    for (int i = 0; i < PW; ++i) piece(i, nk > 1 ? 1 : 0, 1);
+      for (int i = 0; i < PW; ++i) piece(i, nk > 1 ? 1 : 0, 1);
+    }
   }
 
   if constexpr (PRIO == 2)
@@ -195,16 +212,36 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
   if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
 
   // ---------------- epilogue: per-wave 16-row x 64-column slices, 16-B row stores
-  float* ct = reinterpret_cast<float*>(lds) + wave * 16 * CS;
+  // (PERSIST: the slab is the last stage; the others take the next tile's first steps below)
+  float* ct = reinterpret_cast<float*>(lds + (PERSIST ? (STAGES - 1) * STAGE : 0)) + wave * 16 * CS;
   constexpr int CPR = WTN / 4, RPP = 64 / CPR, EB = 16 / RPP;
   const int cc = lane % CPR, rr0 = lane / CPR;
   const int col = n0 + wn * WTN + cc * 4;
   const bool cval = col < p.Co;
+  const int em0 = m0;
   f4 sc4 = {1.f, 1.f, 1.f, 1.f}, bi4 = {0.f, 0.f, 0.f, 0.f}, sl4 = {0.f, 0.f, 0.f, 0.f};
   if (cval) {
     if (p.scale) sc4 = *reinterpret_cast<const f4*>(p.scale + col);
     if (p.bias) bi4 = *reinterpret_cast<const f4*>(p.bias + col);
     if (p.slope) sl4 = *reinterpret_cast<const f4*>(p.slope + col);
+  }
+  if constexpr (PERSIST) {
+    // the next tile's steps 0 and 1, issued after this tile's epilogue constants (one in-order
+    // vmcnt: the compiler's waits for those loads then leave these pieces in flight)
+    pre = t + (int)gridDim.x < p.nwg;
+    if (pre) {
+      setup(t + (int)gridDim.x);
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < PW; ++i) piece(i, 0, 0);
+      if constexpr (STAGES == 3) {
+#pragma unroll
+        for (int i = 0; i < PW; ++i) piece(i, nk > 1 ? 1 : 0, 1);
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
   FrameMax ymax;
 #pragma unroll
@@ -219,7 +256,7 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
     int mm[EB];
 #pragma unroll
     for (int e = 0; e < EB; ++e) {
-      const int m = m0 + wm * (BM / WM) + i * 16 + rr0 + RPP * e;
+      const int m = em0 + wm * (BM / WM) + i * 16 + rr0 + RPP * e;
       mm[e] = m;
       ok[e] = cval && m < p.M;
       res[e] = f4{0.f, 0.f, 0.f, 0.f};
@@ -252,6 +289,10 @@ __global__ __launch_bounds__(512, BM == 128 ? 4 : 1) void conv_gemm_kernel(ConvK
     __builtin_amdgcn_wave_barrier();
   }
   if (p.y_amax) frame_amax_final(p.y_amax, ymax);
+  if constexpr (!PERSIST) break;
+  t += gridDim.x;
+  if (t >= p.nwg) break;
+  }
 }
 
 }  // namespace
@@ -269,7 +310,25 @@ bool conv_gemm_eligible(const ConvK& kp, int prec) {
          !kp.in_scale && !kp.x2 && kp.xsw % 4 == 0;
 }
 
-template <int BN, int WM, int STAGES, int BM = 256, int PRIO = 0, bool EARLY = false>
+// PERSIST: the grid is PRPE_GEMM_PERSIST (default 4) workgroups per CU (one runs at a time per CU:
+// the rest balance the tail when other streams' kernels hold CUs), each walking nwg / grid tiles
+int gemm_persist_grid(int64_t nwg) {
+  static const int per_cu = [] {
+    const char* e = getenv("PRPE_GEMM_PERSIST");
+    const int v = e ? atoi(e) : 4;
+    return v >= 1 && v <= 64 ? v : 4;
+  }();
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    return n > 0 ? n : 256;
+  }();
+  const int64_t g = (int64_t)per_cu * cus / 8 * 8;     // a multiple of 8: t + G stays on t's XCD
+  return (int)(nwg < g ? nwg : g);
+}
+
+template <int BN, int WM, int STAGES, int BM = 256, int PRIO = 0, bool EARLY = false, bool PERSIST = false>
 int launch_gemm(const ConvK& kp0, int prec, hipStream_t st) {
   if (kp0.Co % BN) return PRPE_EINVAL;
   ConvK kp = kp0;
@@ -277,16 +336,19 @@ int launch_gemm(const ConvK& kp0, int prec, hipStream_t st) {
   const int64_t nwg = (int64_t)((kp.M + BM - 1) / BM) * kp.tiles_n;
   if (nwg >= (1LL << 31)) return PRPE_EINVAL;
   kp.nwg = (int)nwg;
-  const dim3 g(kp.nwg), b(512);
-  if (prec == 3) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, true, BM, PRIO, EARLY>), g, b, 0, st, kp);
-  else if (kp.x_planes) hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, true, false, BM, PRIO, EARLY>), g, b, 0, st, kp);
-  else hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, false, BM, PRIO, EARLY>), g, b, 0, st, kp);
+  const dim3 g(PERSIST ? gemm_persist_grid(nwg) : kp.nwg), b(512);
+  if (prec == 3)
+    hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, true, BM, PRIO, EARLY, PERSIST>), g, b, 0, st, kp);
+  else if (kp.x_planes)
+    hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, true, false, BM, PRIO, EARLY, PERSIST>), g, b, 0, st, kp);
+  else
+    hipLaunchKernelGGL((conv_gemm_kernel<BN, WM, STAGES, false, false, BM, PRIO, EARLY, PERSIST>), g, b, 0, st, kp);
   return launch_status();
 }
 
 // tile 40 = auto (256 x 128, 3 stages), 41 = 256 x 256 (2 stages), 42 = 256 x 128 (2 stages),
 // 43 = 128 x 128 (2 stages, two workgroups per CU); 44 / 45 = tile 40 with PRIO 1 / 2, 46 = tile
-// 41 with PRIO 1, 47 / 48 = tiles 41 / 40 with PRIO 1 and EARLY (A/B)
+// 41 with PRIO 1, 48 = tile 40 with PRIO 1 and EARLY (A/B), 47 / 49 = tiles 41 / 40 persistent
 int conv_gemm_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
   switch (tile) {
     case 41: return launch_gemm<256, 2, 2>(kp, prec, st);
@@ -295,8 +357,9 @@ int conv_gemm_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
     case 44: return launch_gemm<128, 4, 3, 256, 1>(kp, prec, st);
     case 45: return launch_gemm<128, 4, 3, 256, 2>(kp, prec, st);
     case 46: return launch_gemm<256, 2, 2, 256, 1>(kp, prec, st);
-    case 47: return launch_gemm<256, 2, 2, 256, 1, true>(kp, prec, st);
+    case 47: return launch_gemm<256, 2, 2, 256, 0, false, true>(kp, prec, st);
     case 48: return launch_gemm<128, 4, 3, 256, 1, true>(kp, prec, st);
+    case 49: return launch_gemm<128, 4, 3, 256, 0, false, true>(kp, prec, st);
     default: return launch_gemm<128, 4, 3>(kp, prec, st);
   }
 }

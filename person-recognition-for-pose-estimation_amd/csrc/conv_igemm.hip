@@ -767,11 +767,11 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     return e && e[0] == '1' ? 1 : e && e[0] == 'a' ? 2 : 0;
   }();
   const bool p3_gemm = prec == 3 && (gemm_p3 == 1 || (gemm_p3 == 2 && kp.K >= 1024 && kp.res_mode == PRPE_RES_NONE));
-  // PRPE_GEMM_TILE=41..48 overrides the automatic GEMM tile (A/B runs)
+  // PRPE_GEMM_TILE=41..49 overrides the automatic GEMM tile (A/B runs)
   static const int gemm_tile = [] {
     const char* e = getenv("PRPE_GEMM_TILE");
     const int t = e ? atoi(e) : 40;
-    return t >= 41 && t <= 48 ? t : 40;
+    return t >= 41 && t <= 49 ? t : 40;
   }();
   // PRPE_GEMM_MIN_KN=<n> keeps GEMMs with K * Co below n on the wave kernel (A/B runs)
   static const int64_t gemm_min_kn = [] {
@@ -783,14 +783,17 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   // the model at bs = 256 (profiles/r05_layer_profile_gemm_tiles.txt): fc1 0.783 -> 0.725 ms,
   // adapter.7 6.71 -> 6.33 ms on 41, while fc2 / proj (residual epilogues) and qkv lose on it
   // (0.636 -> 0.729, 0.220 -> 0.264, 0.526 -> 0.542). PRPE_GEMM_WIDE=0 keeps 40 everywhere (A/B).
+  // The wide tile runs persistent (47: each workgroup walks tiles, the next tile's first K-step
+  // DMA'd under this tile's epilogue): fc1 8.77 -> 8.39 ms over the 12 layers, face-YOLO adapter.7
+  // 6.29 -> 5.94 ms (profiles/r05_gemm_persist.txt); PRPE_GEMM_WIDE=1 keeps the plain 41.
   static const int gemm_wide = [] {
     const char* e = getenv("PRPE_GEMM_WIDE");
-    return e && e[0] == '0' ? 0 : 1;
+    return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 1 : 2;
   }();
   if (tile == 0 && gemm_on && (kp.x_planes || p3_gemm) && kp.M >= (1 << 15) &&
       (int64_t)kp.K * kp.Co >= gemm_min_kn && conv_gemm_eligible(kp, prec)) {
     const bool wide = gemm_wide && gemm_tile == 40 && kp.y_planes && kp.act != PRPE_ACT_NONE && kp.Co % 256 == 0;
-    return conv_gemm_launch(kp, prec, wide ? 41 : gemm_tile, st);
+    return conv_gemm_launch(kp, prec, wide ? (gemm_wide == 2 ? 47 : 41) : gemm_tile, st);
   }
   if (tile >= 30 && tile < 40)
     return conv_halo_eligible(kp, prec, km, tile) ? conv_halo_launch(kp, prec, tile, st) : PRPE_EINVAL;

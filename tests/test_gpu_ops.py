@@ -477,7 +477,7 @@ GEMM_SHAPES = [
 ]
 
 
-@pytest.mark.parametrize("tile", [40, 41, 42, 43])
+@pytest.mark.parametrize("tile", [40, 41, 42, 43, 47, 49])
 @pytest.mark.parametrize("B,Ci,H,W,Co", GEMM_SHAPES)
 def test_conv_gemm_kernel_bit_exact_vs_wave(B, Ci, H, W, Co, tile):
     """conv_gemm.hip (256 x 256 tile, A and B both LDS-DMA'd) == the wave kernel bit for bit:
@@ -509,6 +509,43 @@ def test_conv_gemm_kernel_bit_exact_vs_wave(B, Ci, H, W, Co, tile):
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     assert torch.equal(outs[0][1].cpu(), frame_amax(outs[0][0]))
+
+
+def test_conv_gemm_persistent_walks_many_tiles_bit_exact():
+    """Tiles 49 / 47 (tiles 40 / 41 persistent: each workgroup walks tiles t, t + G, ... with the next
+    tile's first K-steps DMA'd under this tile's epilogue) on a launch with more tiles than workgroups (2 x 399
+    x 401 pixels = 1,250 row tiles x 2 column tiles, the last one ragged) == tile 40 bit for bit:
+    fp32 and planes input, planes and fp32 output, residual, GELU, per-frame max|y|; and at
+    precision 3 (per-row frame scales)."""
+    B, Ci, H, W, Co = 2, 64, 399, 401, 256
+    x = rnd(B, Ci, H, W, seed=290)
+    w = rnd(Co, Ci, 1, 1, seed=291, scale=1.0 / math.sqrt(Ci))
+    sc = torch.rand(Co, generator=_g(292)) + 0.5
+    bi = rnd(Co, seed=293)
+    r = rnd(B, Co, H, W, seed=294)
+    kw = dict(act="gelu", scale=sc, bias=bi, precision=0, res=r, res_mode=RES_PRE)
+    assert torch.equal(run_conv(x, w, 1, 0, tile=49, **kw), run_conv(x, w, 1, 0, tile=40, **kw))
+    assert torch.equal(run_conv(x, w, 1, 0, tile=47, **kw), run_conv(x, w, 1, 0, tile=41, **kw))
+    pk = pack.pack_conv("g", w, 1, 0, DEV, scale=sc, bias=bi, act="gelu")
+    xd = x.permute(0, 2, 3, 1).contiguous().to(DEV)
+    xpl = torch.empty_like(xd)
+    ops.conv2d(xd, pack.pack_conv("i", torch.eye(Ci).view(Ci, Ci, 1, 1), 1, 0, DEV), xpl, precision=2,
+               y_planes=True)
+    outs = []
+    for t in (49, 40):
+        y = torch.empty(B, H, W, Co, device=DEV)
+        ya = torch.zeros(B, device=DEV)
+        ops.conv2d(xpl, pk, y, precision=0, x_planes=True, tile=t, y_amax=ya)
+        ypl = torch.empty(B, H, W, Co, device=DEV)
+        ops.conv2d(xd, pk, ypl, precision=0, y_planes=True, tile=t)
+        outs.append((y, ya, ypl))
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    xr = torch.relu(x) * torch.tensor([7.0, 0.01]).view(B, 1, 1, 1)
+    a, ya = _conv_p3(xr, w, 1, 0, tile=49, scale=sc, bias=bi, act="relu", res=r, res_mode=RES_PRE)
+    b, yb = _conv_p3(xr, w, 1, 0, tile=40, scale=sc, bias=bi, act="relu", res=r, res_mode=RES_PRE)
+    assert torch.equal(a, b) and ya == yb
 
 
 @pytest.mark.parametrize("B,Ci,H,W,Co", GEMM_SHAPES + [(3, 64, 5, 7, 256)])
