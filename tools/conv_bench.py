@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--korders", default="0,1", help="weight K orders to compare (1 = chunk-major)")
     ap.add_argument("--amax", action="store_true", help="also track max|y| (y_amax) in the epilogue")
     ap.add_argument("--act", default="relu", help="epilogue activation (relu, gelu, silu, prelu, none)")
+    ap.add_argument("--y-planes", action="store_true",
+                    help="output in the planes format (y_planes, precision 0), as the model's ViT fc1 / qkv")
     ap.add_argument("--planes", action="store_true",
                     help="input in the planes format (x_planes; precision 0, wave-row kernel)")
     ap.add_argument("--prologue", action="store_true",
@@ -89,7 +91,8 @@ def main():
           for prec in [int(v) for v in a.prec.split(",")]:
             for tile in [int(v) for v in a.tiles.split(",")]:
                 kw = dict(res=r, res_mode=1 if r is not None else 0, precision=prec, tile=tile, y_amax=ya,
-                          x_amax=xa if prec in (3, 4) else None, x_planes=a.planes)
+                          x_amax=xa if prec in (3, 4) else None, x_planes=a.planes,
+                          y_planes=a.y_planes and prec == 0)
                 if a.taps:
                     kw["w2"] = torch.rand(a.taps, Co, device=dev) - 0.5
                     kw["y2"] = torch.empty(B, Ho, Wo, a.taps, device=dev)

@@ -79,7 +79,8 @@ case "$cmd" in
       -- bench.py --config yolo_face --steps 2 --warmup 1 --no-cpu-baseline || exit 12
     bash tools/gpu.sh traffic ${R}_vitpose conv_gemm_kernel 300 764411904 "vit_pose.vit_pose.backbone.encoder.layer.0:fc1" 256 0 \
       conv_gemm.hip,conv.h,common.h "1x1 768->3072 over 49152 tokens, planes input and output, GELU" \
-      -- tools/conv_bench.py --only "vit fc1" --prec 0 --tiles 0 --korders 0 --batch 256 --iters 3 --planes --act gelu || exit 13
+      -- tools/conv_bench.py --only "vit fc1" --prec 0 --tiles 0 --korders 0 --batch 256 --iters 3 --planes --y-planes \
+      --act gelu || exit 13
     # yolo_raw: p1.0 (3x3/2 3->16 on the raw NCHW frames; algorithmic = 64 frames in + the 16-ch map out)
     bash tools/gpu.sh traffic ${R}_yolo_raw "conv_igemm_kernel<128, 16" 300 734004928 yolo_face.yolo.net.p1.0 64 2 \
       conv_igemm.hip,conv.h,common.h "3x3/2 3->16 @640x640, NCHW frames read in place" \
