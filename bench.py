@@ -280,7 +280,13 @@ def main():
                 f"(library's automatic kernel/tile choice, precision {precn})")
         # algorithmic bytes: the input read once, the output written once, the fp32 weights once
         nbytes = 4.0 * (x_numel + pixels * p.co + p.co * p.ci * p.kh * p.kw)
-        if fl / nbytes < MFMA_BF16_PEAK_TFLOPS / HBM_PEAK_GBS * 1e3:      # below the ridge: HBM-bound
+        # the bound: whichever of the two rates the launch runs closer to ITS peak -- HBM bytes / s
+        # against 8 TB/s, or the MFMA work it executes (algorithmic FLOPs x the split's passes)
+        # against the dense bf16 peak (a flop/byte ridge on fp32 bytes called ViT fc1
+        # "hbm" at 1.1 TB/s)
+        hbm_frac = nbytes / avg_s / 1e9 / HBM_PEAK_GBS
+        mfma_exec_frac = fl * passes / avg_s / 1e12 / MFMA_BF16_PEAK_TFLOPS
+        if hbm_frac > mfma_exec_frac:
             ach = nbytes / avg_s / 1e9
             roof = {"bound": "hbm", "kernel": kern, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "algorithmic_gb_per_launch": round(nbytes / 1e9, 4),
@@ -290,6 +296,8 @@ def main():
             roof = {"bound": "mfma", "kernel": kern, "achieved": round(ach, 2), "peak": MFMA_BF16_PEAK_TFLOPS,
                     "unit": "TFLOP/s", "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4),
                     "executed_mfma_passes": passes, "executed_frac": round(ach * passes / MFMA_BF16_PEAK_TFLOPS, 4)}
+        roof.update({"bound_rule": "larger of hbm_frac, mfma_executed_frac", "hbm_frac": round(hbm_frac, 4),
+                     "mfma_executed_frac": round(mfma_exec_frac, 4)})
         roof.update({"avg_launch_ms": round(sum(ms) / len(ms), 4), "launches": len(ms),
                 "measured": ("isolated pass after the timed region (heads sequential)" if isolated
                              else "inside the timed region"),

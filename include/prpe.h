@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define PRPE_ABI_VERSION 9
+#define PRPE_ABI_VERSION 10
 
 /* activations (epilogues/prologues) */
 enum prpe_act {
@@ -241,41 +241,6 @@ int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t align_corners
                    const float* scale, const float* bias, const float* slope, int32_t act,
                    int32_t y_planes, float* y_amax, void* workspace, int64_t workspace_bytes,
                    void* stream);
-
-/*
- * Upsample-fused 1x1 GEMM (ABI 9): prpe_upconv3x3 (above) followed by a 1x1 conv as ONE launch,
- *   u = up_act(upconv3x3(z) * up_scale + up_bias)        (never written to memory)
- *   y = act((W u) * scale + bias)
- * the face-YOLO adapter's .4 (bilinear upsample + 3x3 + BN + SiLU) and .7 (1x1 512 -> 256 + BN +
- * SiLU), modify_models.py:47-56. z: [N, Hi, Wi, 9 C] tap maps as prpe_upconv3x3's (C % 32 == 0),
- * channel-contiguous, 16-B aligned; y: [N, Ho, Wo, 256] channel-contiguous, 32-B aligned, pixel
- * strides multiples of 8 floats. W: the 1x1's precision-0 pack (bf16 planes w_hi / w_lo
- * [256][k_pad], k_pad >= C, K order = channel order), scale / bias / slope [256] (optional), act.
- * The upconv epilogue: up_scale / up_bias [C] (required), up_slope (optional), up_act.
- * y_planes: y in the planes format (prpe_conv_desc) for a precision-0 consumer. Every 16-pixel
- * run of output rows / columns must map to at most 5 source rows / columns (the LDS window:
- * upsampling ratios >= ~4, e.g. 20 -> 160), one frame of z < 2^31 bytes, y not overlapping z;
- * anything else returns -EINVAL. Bit-identical to prpe_upconv3x3 (y_planes) + prpe_conv2d
- * (precision 0, planes input) on the same operands.
- */
-typedef struct prpe_upgemm_desc {
-  prpe_view z;
-  prpe_view y;
-  int32_t align_corners;
-  const float* up_scale;
-  const float* up_bias;
-  const float* up_slope;
-  int32_t up_act;
-  const uint16_t* w_hi;
-  const uint16_t* w_lo;
-  int32_t k_pad;
-  const float* scale;
-  const float* bias;
-  const float* slope;
-  int32_t act;
-  int32_t y_planes;
-} prpe_upgemm_desc;
-int prpe_upconv_gemm(const prpe_upgemm_desc* d, void* stream);
 
 /* Depthwise kxk conv (groups = C) + folded BN + act (+ post-act residual add when res.ptr).
  * Replaces yolopt Conv(g=ch) (nn.py:108, :248-250). */

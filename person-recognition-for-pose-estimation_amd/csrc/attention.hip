@@ -912,6 +912,14 @@ int attention_launch(const float* qkv, AttnStrides sd, float* out, int32_t B, in
   if (!qkv || !out || B <= 0 || H <= 0 || L != AL || D != AD) return PRPE_EINVAL;
   if ((uintptr_t)qkv % 16 || (uintptr_t)out % 16) return PRPE_EINVAL;
   if (sd.frame % 4 || sd.which % 4 || sd.head % 4 || sd.tok % 4) return PRPE_EINVAL;
+  // negative strides are not a layout this entry point takes (prpe.h); the whole-head kernel
+  // addresses a frame through one buffer descriptor with 32-bit offsets, so it only takes frames
+  // whose q / k / v extent (and therefore every per-thread and scalar offset inside it) is below
+  // 2^31 bytes -- a frame-interleaved layout (s_tok = B * 3HD, ...) beyond that goes to the
+  // streaming kernel, which addresses with 64-bit pointers
+  if (sd.frame < 0 || sd.which < 0 || sd.head < 0 || sd.tok < 0) return PRPE_EINVAL;
+  const int64_t frame_extent = ((int64_t)(L - 1) * sd.tok + 2 * sd.which + (int64_t)(H - 1) * sd.head + D) * 4;
+  const bool desc_ok = frame_extent < (1LL << 31);
   // PRPE_ATTN selects the kernel for A/B runs: 1 = the round-1 kernel (P through LDS, all 192
   // keys staged, 12 waves), KC*10 + QT = transposed kernel with KC-key chunks and QT query tiles
   // per wave (322, 641, 642, 962); 32 / 64 / 96 = the streaming kernel with that chunk;
@@ -932,11 +940,11 @@ int attention_launch(const float* qkv, AttnStrides sd, float* out, int32_t B, in
   const dim3 gs(B * H / hpw);
   if (out_planes) {
     if ((uintptr_t)out % 32) return PRPE_EINVAL;
-    if (sel == 4) hipLaunchKernelGGL((vit_attention_h_kernel<true>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale);
+    if (sel == 4 && desc_ok) hipLaunchKernelGGL((vit_attention_h_kernel<true>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale);
     else hipLaunchKernelGGL((vit_attention_s_kernel<64, true>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale);
     return launch_status();
   }
-  if (sel == 4) {
+  if (sel == 4 && desc_ok) {
     hipLaunchKernelGGL((vit_attention_h_kernel<false>), gs, dim3(NWAVE * 64), 0, st, qkv, sd, out, H, hpw, scale);
     return launch_status();
   }

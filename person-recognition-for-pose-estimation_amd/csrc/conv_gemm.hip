@@ -313,18 +313,18 @@ bool conv_gemm_eligible(const ConvK& kp, int prec) {
 // PERSIST: the grid is PRPE_GEMM_PERSIST (default 4) workgroups per CU (one runs at a time per CU:
 // the rest balance the tail when other streams' kernels hold CUs), each walking nwg / grid tiles
 int gemm_persist_grid(int64_t nwg) {
-  static const int per_cu = [] {
-    const char* e = getenv("PRPE_GEMM_PERSIST");
-    const int v = e ? atoi(e) : 4;
-    return v >= 1 && v <= 64 ? v : 4;
-  }();
+  // 4 workgroups per CU (round 5's sweep of 2 / 4 / 8 / 16 was flat, profiles/r05_gemm_persist.txt)
+  constexpr int per_cu = 4;
   static const int cus = [] {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       n = 256;
     return n > 0 ? n : 256;
   }();
-  const int64_t g = (int64_t)per_cu * cus / 8 * 8;     // a multiple of 8: t + G stays on t's XCD
+  // a multiple of 8 (t + G stays on t's XCD), and at least 8: a device (or partition) with fewer
+  // than two CUs would otherwise round the grid down to 0 workgroups
+  int64_t g = (int64_t)per_cu * cus / 8 * 8;
+  if (g < 8) g = 8;
   return (int)(nwg < g ? nwg : g);
 }
 

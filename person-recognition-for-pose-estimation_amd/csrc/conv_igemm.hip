@@ -727,15 +727,10 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     else hipLaunchKernelGGL((conv_smallco_kernel<4, 1>), dim3(blocks), dim3(256), 0, st, kp, lg);
     return launch_status();
   }
-  // direct global->LDS kernel (conv_glds.hip) for chunked inputs with Co > 32: tile 10..12
-  // forces one of its tiles; PRPE_CONV_GLDS=1 in the environment makes it the automatic
-  // choice for two-plane Co <= 64 convs again. Off by default: this file's 256x64 tile now
-  // measures 27 % faster on those shapes in isolation (profiles/r01_conv_bench_sweep_v4.txt)
-  // and -0.6..1.0 ms per sequential forward (AdaFace / YOLO adapter 64-channel convs).
-  static const int glds_on = [] {
-    const char* e = getenv("PRPE_CONV_GLDS");
-    return e && e[0] == '1' ? 1 : 0;
-  }();
+  // direct global->LDS kernel (conv_glds.hip) for chunked inputs with Co > 32: tiles 10..12 only
+  // (never the automatic choice since round 1: this file's 256x64 tile measures 27 % faster on
+  // its shapes in isolation, profiles/r01_conv_bench_sweep_v4.txt, and -0.6..1.0 ms per
+  // sequential forward; the round-1 environment switch back to it was removed in round 6)
   static const int wave_on = [] {
     const char* e = getenv("PRPE_CONV_WAVE");
     return e && e[0] == '0' ? 0 : 1;
@@ -773,11 +768,6 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     const int t = e ? atoi(e) : 40;
     return t >= 41 && t <= 49 ? t : 40;
   }();
-  // PRPE_GEMM_MIN_KN=<n> keeps GEMMs with K * Co below n on the wave kernel (A/B runs)
-  static const int64_t gemm_min_kn = [] {
-    const char* e = getenv("PRPE_GEMM_MIN_KN");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
   // the 256 x 256 tile (41) for the GEMMs that write the planes format through an activation
   // (ViT fc1: GELU, face-YOLO adapter.7: SiLU), the 256 x 128 one (40) for the rest: measured in
   // the model at bs = 256 (profiles/r05_layer_profile_gemm_tiles.txt): fc1 0.783 -> 0.725 ms,
@@ -791,7 +781,7 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
     return e && e[0] == '0' ? 0 : e && e[0] == '1' ? 1 : 2;
   }();
   if (tile == 0 && gemm_on && (kp.x_planes || p3_gemm) && kp.M >= (1 << 15) &&
-      (int64_t)kp.K * kp.Co >= gemm_min_kn && conv_gemm_eligible(kp, prec)) {
+      conv_gemm_eligible(kp, prec)) {
     const bool wide = gemm_wide && gemm_tile == 40 && kp.y_planes && kp.act != PRPE_ACT_NONE && kp.Co % 256 == 0;
     return conv_gemm_launch(kp, prec, wide ? (gemm_wide == 2 ? 47 : 41) : gemm_tile, st);
   }
@@ -811,7 +801,6 @@ extern "C" int prpe_conv2d(const prpe_conv_desc* d, void* stream) {
   // 256x64 tile measured faster (profiles/r01_conv_bench_wave.txt, r01_conv_bench_sweep_v4.txt)
   if (tile == 0 && wave_on && y.c > 32 && (prec == 2 || y.c > 64) && conv_wave_eligible(kp, prec, km))
     return conv_wave_launch(kp, prec, 20, st);
-  if (tile == 0 && glds_on && y.c > 32 && conv_glds_eligible(kp, prec, km)) return conv_glds_launch(kp, prec, 0, st);
   // measured (tools/conv_bench.py, profiles/r01_conv_bench_tiles.txt): the 3-plane mode wants the
   // 256x128 8-wave tile for wide Co (operand traffic per MFMA halves; +30%), 128x64 below;
   // the 2-plane mode is near-flat between 128x128 and 256x128 (256x128 +2% on 3x3) and

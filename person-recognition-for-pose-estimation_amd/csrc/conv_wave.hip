@@ -549,19 +549,10 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       const char* e = getenv("PRPE_WAVE_WIDE");
       return e ? atoi(e) : 28;
     }();
-    // PRPE_WAVE_P3_NARROW=<tile> overrides the precision-3 short-K / narrow choice (A/B runs)
-    static const int p3_narrow = [] {
-      const char* e = getenv("PRPE_WAVE_P3_NARROW");
-      return e ? atoi(e) : 25;
-    }();
-    // precision 3 with Co > 64 takes the wide tile at any K: the short-K residual GEMMs of the
-    // trunk (conv3 + residual, K = 64 / 128 / dual 128) run 16-19 % faster on it than on the
-    // 256 x 64 tile at bs = 256 (profiles/r01_conv_bench_sweep_v4.txt; bench +1.2 %);
-    // PRPE_WAVE_P3_SMALLK=0 restores the 256 x 64 tile for K <= 128 (A/B runs)
-    static const int p3_smallk_wide = [] {
-      const char* e = getenv("PRPE_WAVE_P3_SMALLK");
-      return e && e[0] == '0' ? 0 : 1;
-    }();
+    // precision 3: Co <= 64 on the 256 x 64 tile (25); Co > 64 on the wide tile at any K: the
+    // short-K residual GEMMs of the trunk (conv3 + residual, K = 64 / 128 / dual 128) run 16-19 %
+    // faster on it than on the 256 x 64 tile at bs = 256 (profiles/r01_conv_bench_sweep_v4.txt;
+    // bench +1.2 %). (The round-1/2 A/B switches of both choices were removed in round 6.)
     // precision 3, Co > 64: the 256 x 128 8-wave tile (wave 32 x 128, 3-stage ring) since round 4:
     // trunk convs 68.6 -> 66.1 ms at bs = 256 against the 128 x 128 2-stage tile, every unfused
     // trunk conv faster (profiles/r04_layer_profile_trunk_wide3_sweep.txt; round 2 had measured the
@@ -580,7 +571,7 @@ int conv_wave_launch(const ConvK& kp, int prec, int tile, hipStream_t st) {
       return e ? atoi(e) : 27;
     }();
     if (prec == 0) tile = wide;
-    else if (prec == 3) tile = kp.Co > 64 && (kp.K > 128 || p3_smallk_wide) ? wide3 : p3_narrow;
+    else if (prec == 3) tile = kp.Co > 64 ? wide3 : 25;
     else if (prec == 4) tile = kp.Co > 64 ? wide4 : 25;  // (the precision-3 overrides do not apply)
     else tile = kp.Co > 64 && kp.K > 128 ? tile2 : 24;
   }

@@ -27,6 +27,19 @@ __device__ __forceinline__ float lerp_add(float x, float l, float a, float b) {
   return r;
 }
 
+// lerp_add on two channels as packed FP32 math (v_pk_mul_f32 l b, v_pk_fma_f32 (1 - l) a + l b,
+// v_pk_add_f32; the scalar l / 1 - l broadcast by op_sel): per lane exactly lerp_add's three IEEE
+// operations in the same order, so the packed and scalar forms are bit-identical. Contraction is
+// off here so the add is not re-fused with the product (fadd(fma(m, a, l b), x) ->
+// fma(m, a, fma(l, b, x)) is legal under contraction).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v lerp_add2(f2v x, float l, f2v a, f2v b) {
+#pragma clang fp contract(off)
+  const float ml = 1.f - l;
+  const f2v lb = l * b;
+  return x + __builtin_elementwise_fma(f2v{ml, ml}, a, lb);
+}
+
 // PyTorch upsample_bilinear2d source index (aten/src/ATen/native/UpSample.h semantics):
 // align_corners: src = dst * (in-1)/(out-1); else src = max(0, (dst+0.5)*in/out - 0.5).
 __device__ __forceinline__ void bilin_src(int dst, int in, int out, int ac, int& i0, int& i1, float& l1) {
@@ -349,18 +362,29 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
     bi[v] = p.bias ? p.bias[c] : 0.f;
     sl[v] = p.slope ? p.slope[c] : 0.f;
   }
-  auto hrow = [&](int r, int dy, float (&h)[4]) {
-    const float* rr = ring[r % UPD_RING] + dy * 3 * 32;
-#pragma unroll
-    for (int v = 0; v < 4; ++v) h[v] = 0.f;
-#pragma unroll
-    for (int dx = 0; dx < 3; ++dx) {
-      if (!((xvalid >> dx) & 1u)) continue;
-      const f32x4 A = *reinterpret_cast<const f32x4*>(rr + lo[dx]);
-      const f32x4 B = *reinterpret_cast<const f32x4*>(rr + l1[dx]);
-#pragma unroll
-      for (int v = 0; v < 4; ++v) h[v] = lerp_add(h[v], lx[dx], A[v], B[v]);
-    }
+  // The ring reads are inline asm (all six of an H row, one lgkmcnt wait): as plain loads the
+  // compiler put `s_waitcnt vmcnt(0)` before every one of them (an LDS read after an LDS-DMA it
+  // cannot tell apart waits for the youngest DMA), i.e. each H-row rebuild drained every store
+  // the wave had in flight -- the serialisation this kernel exists to avoid. The rows read here
+  // are covered by the counted `vmcnt` + barrier at the event that brought them into use (see
+  // above); a column outside the image reads an in-ring address (x0 = x1 = xs_lo) and skips its
+  // lerp, as before.
+  const unsigned ring_lds = (unsigned)(uintptr_t)(lds_ptr_t)&ring[0][0];
+  auto hrow = [&](int r, int dy, f2v (&h)[2]) {
+    const unsigned rr = ring_lds + (unsigned)(((r % UPD_RING) * UPD_NI * 256 + dy * 3 * 32) * 4);
+    f32x4 A0, B0, A1, B1, A2, B2;
+    asm volatile(
+        "ds_read_b128 %0, %6\n\tds_read_b128 %1, %7\n\tds_read_b128 %2, %8\n\t"
+        "ds_read_b128 %3, %9\n\tds_read_b128 %4, %10\n\tds_read_b128 %5, %11\n\ts_waitcnt lgkmcnt(0)"
+        : "=&v"(A0), "=&v"(B0), "=&v"(A1), "=&v"(B1), "=&v"(A2), "=&v"(B2)
+        : "v"(rr + lo[0] * 4), "v"(rr + l1[0] * 4), "v"(rr + lo[1] * 4), "v"(rr + l1[1] * 4), "v"(rr + lo[2] * 4),
+          "v"(rr + l1[2] * 4));
+    f2v h0 = {0.f, 0.f}, h1 = {0.f, 0.f};
+    if (xvalid & 1u) { h0 = lerp_add2(h0, lx[0], A0.xy, B0.xy); h1 = lerp_add2(h1, lx[0], A0.zw, B0.zw); }
+    if (xvalid & 2u) { h0 = lerp_add2(h0, lx[1], A1.xy, B1.xy); h1 = lerp_add2(h1, lx[1], A1.zw, B1.zw); }
+    if (xvalid & 4u) { h0 = lerp_add2(h0, lx[2], A2.xy, B2.xy); h1 = lerp_add2(h1, lx[2], A2.zw, B2.zw); }
+    h[0] = h0;
+    h[1] = h1;
   };
   __syncthreads();                                    // the row tables
   // rows in use for output row oy: [y0 of row oy-1 (or oy), y1 of row oy+1]; hi_at = the top one
@@ -395,7 +419,7 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
   // wave-uniform parity bit says (par 0: A = h0, B = h1): moving down one source row flips the
   // parity and refills the old A slot, so no register copies (the hA = hB rolling form made the
   // compiler move 8 registers per dy and row on every path)
-  float h0[3][4], h1[3][4];
+  f2v h0[3][2], h1[3][2];
   int cur[3] = {-2, -2, -2};
   int par[3] = {0, 0, 0};
   float ym = 0.f;
@@ -411,7 +435,7 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
       in_use = need;
       while (issued < need + 1 && issued + 1 < Hi) issue_row(++issued);   // one row ahead again
     }
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    f2v acc[2] = {{0.f, 0.f}, {0.f, 0.f}};
 #pragma unroll
     for (int dy = 0; dy < 3; ++dy) {
       const int y0 = __builtin_amdgcn_readfirstlane(ty0[oy - oy0 + dy]);
@@ -433,16 +457,16 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
       }
       if (par[dy]) {
 #pragma unroll
-        for (int v = 0; v < 4; ++v) acc[v] = lerp_add(acc[v], ly, h1[dy][v], h0[dy][v]);
+        for (int q = 0; q < 2; ++q) acc[q] = lerp_add2(acc[q], ly, h1[dy][q], h0[dy][q]);
       } else {
 #pragma unroll
-        for (int v = 0; v < 4; ++v) acc[v] = lerp_add(acc[v], ly, h0[dy][v], h1[dy][v]);
+        for (int q = 0; q < 2; ++q) acc[q] = lerp_add2(acc[q], ly, h0[dy][q], h1[dy][q]);
       }
     }
     if (!live) continue;
     f32x4 pre;
 #pragma unroll
-    for (int v = 0; v < 4; ++v) pre[v] = acc[v] * sc[v] + bi[v];
+    for (int v = 0; v < 4; ++v) pre[v] = acc[v >> 1][v & 1] * sc[v] + bi[v];
     const f32x4 o4 = apply_act4(pre, ACT >= 0 ? ACT : p.act, f32x4{sl[0], sl[1], sl[2], sl[3]});
     const float out[4] = {o4[0], o4[1], o4[2], o4[3]};
     ym = fmaxf(ym, amax4(o4));
@@ -1034,11 +1058,7 @@ extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t al
   if (span(z) >= (1LL << 31) || span(y) >= (1LL << 31) || z->sw < 0 || z->sc < 0 || z->sh < 0 || y->sw < 0 ||
       y->sc < 0)
     return PRPE_EINVAL;
-  static const int xcd_env = [] {
-    const char* e = getenv("PRPE_UPCONV_XCD");
-    return e ? atoi(e) : 1;
-  }();
-  p.xcd = xcd_env;
+  p.xcd = 1;   // XCD-contiguous block order (round 2: -12..27 % per launch; its A/B switch removed in round 6)
   const dim3 g((unsigned)nb);
   static const int abl = [] {
     const char* e = getenv("PRPE_UPCONV_ABL");

@@ -14,7 +14,7 @@ from ._srchash import source_hash
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libprpe.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 
 class PrpeError(RuntimeError):
@@ -57,13 +57,6 @@ class StemDesc(C.Structure):
                 ("y_amax", C.c_void_p)]
 
 
-class UpGemmDesc(C.Structure):
-    _fields_ = [("z", View), ("y", View), ("align_corners", C.c_int32), ("up_scale", C.c_void_p),
-                ("up_bias", C.c_void_p), ("up_slope", C.c_void_p), ("up_act", C.c_int32), ("w_hi", C.c_void_p),
-                ("w_lo", C.c_void_p), ("k_pad", C.c_int32), ("scale", C.c_void_p), ("bias", C.c_void_p),
-                ("slope", C.c_void_p), ("act", C.c_int32), ("y_planes", C.c_int32)]
-
-
 ACT = {"none": 0, "relu": 1, "silu": 2, "prelu": 3, "gelu": 4, "sigmoid": 5}
 RES_NONE, RES_PRE, RES_POST = 0, 1, 2
 
@@ -77,7 +70,6 @@ SIGNATURES = {
     "prpe_conv2d_workspace_bytes": (C.c_int64, [C.POINTER(ConvDesc)]),
     "prpe_conv2d": (C.c_int, [C.POINTER(ConvDesc), _P]),
     "prpe_bottleneck": (C.c_int, [C.POINTER(BneckDesc), _P]),
-    "prpe_upconv_gemm": (C.c_int, [C.POINTER(UpGemmDesc), _P]),
     "prpe_stem_maxpool": (C.c_int, [C.POINTER(StemDesc), _P]),
     "prpe_upconv3x3_workspace_bytes": (C.c_int64, [_VP, _VP]),
     "prpe_upconv3x3": (C.c_int, [_VP, _VP, _I, _P, _P, _P, _I, _I, _P, _P, _L, _P]),

@@ -83,12 +83,6 @@ BNECK_L2 = os.environ.get("PRPE_BNECK_L2", "1") != "0"
 # stem conv + max-pool as ONE launch (prpe_stem_maxpool: the [B, 320, 320, 64] stem map stays in
 # LDS); PRPE_STEM_POOL=0 runs prpe_conv2d + prpe_maxpool
 STEM_POOL = os.environ.get("PRPE_STEM_POOL", "1") != "0"
-# face-YOLO adapter .4 (upsample + 3x3 + BN + SiLU) and .7 (1x1 + BN + SiLU) as ONE launch
-# (prpe_upconv_gemm, round 5: the 512-channel 160x160 map never reaches HBM) with PRPE_UPGEMM=1;
-# bit-identical to prpe_upconv3x3 + prpe_conv2d but measured slower (12.48 ms vs 6.26 ms + the
-# upconv at bs = 256, profiles/r05_upgemm_ab.txt: its upsample prologue runs serialised with the
-# MFMAs), so the default stays unfused
-UPGEMM = os.environ.get("PRPE_UPGEMM", "0") == "1"
 
 
 class _Prec:
@@ -126,6 +120,7 @@ class Engine:
         self._aux: dict[str, torch.Tensor] = {}
         self.watch: set[str] = set()      # pack names whose launches get HIP-event timing
         self.events: dict[str, list] = {}
+        self.up_events: dict[str, list] = {}   # upconv launches (tools/layer_profile.py), when watched
         # per-component device pools of per-frame max|y| slots (precision 3): comp -> [chunk
         # tensors, cursor (chunk index, offset)]
         self._amax_pools: dict[str, list] = {}
@@ -306,42 +301,18 @@ class Engine:
         planes = PLANES_ON and planes and self.precision == 0 and co % 8 == 0 and out.is_contiguous()
         # a precision-3/4 consumer reads the output's per-frame max|y| as its activation scale
         ya = self.amax_slot(B) if self.precision in F16_PRECS else None
-        ops.upconv3x3(z, out, align_corners, self._aux[key], self._aux[key + "b"], slope, act, y_planes=planes,
-                      y_amax=ya)
+        args = (z, out, align_corners, self._aux[key], self._aux[key + "b"], slope, act)
+        if name + ":upconv" in self.watch:     # HIP events around the launch (tools/layer_profile.py)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            ops.upconv3x3(*args, y_planes=planes, y_amax=ya)
+            e1.record()
+            self.up_events.setdefault(name, []).append((e0, e1, out.numel() * 4, z.numel() * 4, planes, act))
+        else:
+            ops.upconv3x3(*args, y_planes=planes, y_amax=ya)
         out._prpe_amax = ya
         if planes:
             out._prpe_planes = True
-        return out
-
-    def upconv_gemm(self, name, x, wkey, size, align_corners, p1x1, bn=None, bias_key=None, act="none"):
-        """``upconv`` (planes output) followed by the 1x1 ``p1x1`` (precision 0, planes output) as ONE
-        launch (prpe_upconv_gemm): the upsampled map never reaches HBM. Same bits as the two calls."""
-        taps = self._packs.get(name + ":taps")
-        if taps is None:
-            taps = pack_upconv_taps(name + ":taps", self.sd[wkey], self.device)
-            self._packs[name + ":taps"] = taps
-        co = taps.co // 9
-        key = name + ":epi"
-        if key not in self._aux:
-            cb = self.sd[bias_key] if bias_key else None
-            if bn is not None:
-                s, b = bn_affine(self.sd, bn, BN_EPS, cb)
-            else:
-                s, b = torch.ones(co), (cb if cb is not None else torch.zeros(co))
-            self._aux[key] = s.float().to(self.device)
-            self._aux[key + "b"] = b.float().contiguous().to(self.device)
-        z = self.conv(x, taps)
-        out = self.empty(z.shape[0], size[0], size[1], p1x1.co)
-        if p1x1.name in self.watch:       # HIP events around one kernel (bench roofline)
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-        ops.upconv_gemm(z, p1x1, out, align_corners, self._aux[key], self._aux[key + "b"], up_act=act, y_planes=True)
-        if p1x1.name in self.watch:
-            e1.record()
-            self.events.setdefault(p1x1.name, []).append((e0, e1, out.shape[0] * size[0] * size[1], p1x1, 0,
-                                                          z.numel()))
-        out._prpe_amax = None
-        out._prpe_planes = True
         return out
 
     def conv3x3_smallco(self, x, name, wkey, bn=None, bias_key=None, act="none"):
@@ -575,13 +546,9 @@ class Engine:
         t = self.conv(feat, self.pk(a + ".0", a + ".0.weight", bn=a + ".1", bias_key=a + ".0.bias", act="silu"),
                       prec=self.feat_prec(feat))
         p7 = self.pk(a + ".7", a + ".7.weight", bn=a + ".8", bias_key=a + ".7.bias", act="silu")
-        if UPGEMM and self.precision == 0 and PLANES_ON:
-            t = self.upconv_gemm(a + ".4", t, a + ".4.weight", (160, 160), True, p7, bn=a + ".5",
-                                 bias_key=a + ".4.bias", act="silu")
-        else:
-            u = self.upconv(a + ".4", t, a + ".4.weight", (160, 160), True, bn=a + ".5", bias_key=a + ".4.bias",
-                            act="silu", planes=True)
-            t = self.conv(u, p7, planes_out=True)
+        u = self.upconv(a + ".4", t, a + ".4.weight", (160, 160), True, bn=a + ".5", bias_key=a + ".4.bias",
+                        act="silu", planes=True)
+        t = self.conv(u, p7, planes_out=True)
         p10 = self.pk(a + ".10", a + ".10.weight", 1, 1, bn=a + ".11", bias_key=a + ".10.bias", act="silu")
         if SMALLCO_TAPS and TAPS_FUSE and getattr(t, "_prpe_planes", False):
             # .10's epilogue runs .13 (1x1 128->64 + BN + SiLU) and .16's tap GEMM (64 -> 27):

@@ -44,8 +44,9 @@ def pose_flip_test(model, images, mode: str = "reference"):
     """Averaged flip-test heatmaps [B,17,64,48] for ``images`` [B,3,H,W] (module.py:466-484)."""
     if mode not in ("reference", "swap"):
         raise ValueError(f"unknown flip mode {mode!r}")
-    e = model.engine
     x = model._check_input(images)
+    model._sync_weights()                         # repack if a weight changed in place
+    e = model.engine
     heat = e.vitpose(e.trunk(x))
     heat_f = e.vitpose(e.trunk(x, flip_w=True))
     return ops.flip_average(heat, heat_f, flip_partner(heat.shape[1]), 0 if mode == "reference" else 1)
@@ -64,7 +65,10 @@ class FaceRecognitionEval:
         self.set_kernel(kernel)
 
     def set_kernel(self, kernel):
-        """Normalise + pack the [512, classes] head kernel (call again after it changes)."""
+        """Normalise + pack the [512, classes] head kernel. An in-place change of ``kernel``
+        (the model's ``ada_face.head.kernel`` parameter) is detected by its version counter at
+        the next call and repacked, as ``CombinedModel`` does for its weights."""
+        self._kernel, self._kernel_version = kernel, kernel._version
         k = kernel.to(self.model.device, torch.float32).contiguous()
         d, ncls = k.shape
         kn = torch.empty_like(k)
@@ -74,6 +78,8 @@ class FaceRecognitionEval:
                                 scale=torch.full((ncls,), self.s))
 
     def logits(self, embeddings):
+        if self._kernel._version != self._kernel_version:
+            self.set_kernel(self._kernel)
         B, d = embeddings.shape
         e = embeddings.contiguous().float()
         en = torch.empty_like(e)

@@ -6,6 +6,10 @@ Same surface the eval steps touch:
     per-task types: detection -> Tensor [B, 4+1, 525]; pose -> object with ``.heatmaps``
     [B,17,64,48]; face_recognition -> (embeddings [B,512], norms [B,1]);
   * ``state_dict()/load_state_dict()`` with the reference's 2130 keys;
+  * parameters stay live: an in-place change through ``parameters()`` / ``state_dict()`` (an
+    optimizer step in ``pl.Trainer.fit``, round_robin_trainer.py:258-262, before validation)
+    is seen at the next call and the engine repacks (``_sync_weights``), so a forward never
+    computes with stale packed weights;
   * ``model.yolo_face.yolo.head.stride`` / ``yolo_person...`` (a fresh ``Head`` after
     ``modify_yolo`` has stride zeros, nn.py:238 -> eval boxes are 0; honoured as given);
   * ``model.ada_face.head.kernel`` for the face-recognition eval logits;
@@ -68,7 +72,35 @@ class CombinedModel:
         for b, st in strides.items():          # a reload keeps the stride the caller set
             getattr(self, b).yolo.head.stride = st
         self.engine = Engine(self._sd, self.device, self.precision)
+        self._mark_packed()
         return SimpleNamespace(missing_keys=missing, unexpected_keys=unexpected)
+
+    # ------------------------------------------------------------------ weight freshness
+    # The HIP engine computes from packed device copies of ``_sd`` (split planes, folded BN).
+    # Every tensor the caller can reach -- the branch trees' parameters / buffers, the trunk's
+    # ``parameters()``, ``state_dict()`` values -- shares storage AND autograd's version counter
+    # with its ``_sd`` entry (nn.Parameter(t) / t.detach() alias t), so any in-place write through
+    # them (``p.add_``, ``p.copy_``, an optimizer step) bumps that entry's ``_version``. The
+    # versions are recorded when the engine packs; every entry point compares them first and
+    # repacks on a change. (``p.data.<op>_`` bypasses the version counter by PyTorch's design:
+    # call ``refresh_weights()`` after such writes.)
+    def _mark_packed(self):
+        self._packed = [(t, t._version) for t in self._sd.values()]
+
+    def weights_stale(self) -> bool:
+        """True if a state_dict tensor changed in place since the engine packed it."""
+        return any(t._version != v for t, v in getattr(self, "_packed", ()))
+
+    def refresh_weights(self):
+        """Repack every weight from the (possibly edited) state_dict tensors."""
+        self.engine = Engine(self._sd, self.device, self.precision)
+        self._mark_packed()
+
+    def _sync_weights(self):
+        if self.engine is None:
+            raise RuntimeError("no weights loaded: call load_state_dict first")
+        if self.weights_stale():
+            self.refresh_weights()
 
     def state_dict(self):
         return dict(self._sd)
@@ -117,6 +149,7 @@ class CombinedModel:
     @torch.no_grad()
     def forward(self, x):
         x = self._check_input(x)
+        self._sync_weights()
         e = self.engine
         feat = e.trunk(x)
         t = self.current_task
@@ -139,6 +172,7 @@ class CombinedModel:
         if not (isinstance(x, torch.Tensor) and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4
                 and tuple(x.shape[1:]) == (3,) + tuple(arch.VIT_IMG)):
             raise ValueError(f"expected float32 CUDA(HIP) pixel_values [B,3,{arch.VIT_IMG[0]},{arch.VIT_IMG[1]}]")
+        self._sync_weights()
         e = self.engine
         with e.prec("vit"):
             return PoseOutput(heatmaps=e.vit_backbone(ops.nhwc(x)))
@@ -151,6 +185,7 @@ class CombinedModel:
         x = self._check_input(x)
         if x.shape[2] % 32 or x.shape[3] % 32:
             raise ValueError("YOLO input H and W must be multiples of 32 (the P5 stride)")
+        self._sync_weights()
         return self.engine.yolo_raw(branch, x, self._stride(getattr(self, branch)))
 
     @torch.no_grad()
@@ -163,6 +198,7 @@ class CombinedModel:
         other heads' MFMA-bound convs, and one kernel's tail wave no longer idles the chip.
         Same kernels, same arithmetic: results are bit-identical to the sequential order."""
         x = self._check_input(x)
+        self._sync_weights()
         e = self.engine
         feat = e.trunk(x)
         stride = face_stride if face_stride is not None else self._stride(self.yolo_face)

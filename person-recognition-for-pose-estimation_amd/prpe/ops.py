@@ -10,7 +10,7 @@ import ctypes as C
 
 import torch
 
-from ._lib import ACT, RES_NONE, BneckDesc, ConvDesc, PrpeError, StemDesc, UpGemmDesc, View, check, lib
+from ._lib import ACT, RES_NONE, BneckDesc, ConvDesc, PrpeError, StemDesc, View, check, lib
 
 
 def _stream() -> C.c_void_p:
@@ -175,26 +175,6 @@ def upconv3x3(z, y, align_corners, scale=None, bias=None, slope=None, act="none"
     check(lib().prpe_upconv3x3(C.byref(zv), C.byref(yv), 1 if align_corners else 0, _ptr(scale), _ptr(bias),
                                _ptr(slope), ACT[act], int(y_planes), _ptr(y_amax), _ptr(ws), nbytes, _stream()),
           "prpe_upconv3x3")
-    return y
-
-
-def upconv_gemm(z, pack, y, align_corners, up_scale, up_bias, up_slope=None, up_act="none", act=None,
-                y_planes=False):
-    """prpe_upconv_gemm (include/prpe.h): upconv3x3(z) + its BN / act, then the 1x1 ``pack``
-    (precision 0) + its epilogue, in one launch -- the upsampled map never reaches memory.
-    Bit-identical to ``upconv3x3(..., y_planes=True)`` followed by ``conv2d(..., x_planes=True)``."""
-    _gpu(z, y, pack.w_hi, up_scale, up_bias)
-    if pack.kh != 1 or pack.kw != 1 or pack.k_order != 0 or pack.ci * 9 != z.shape[3]:
-        raise ValueError(f"prpe_upconv_gemm[{pack.name}]: needs a 1x1 pack over the {z.shape[3] // 9} upconv channels")
-    d = UpGemmDesc()
-    d.z, d.y = view(z), view(y)
-    d.align_corners = 1 if align_corners else 0
-    d.up_scale, d.up_bias, d.up_slope, d.up_act = _ptr(up_scale), _ptr(up_bias), _ptr(up_slope), ACT[up_act]
-    d.w_hi, d.w_lo, d.k_pad = pack.w_hi.data_ptr(), pack.w_lo.data_ptr(), pack.k_pad
-    d.scale, d.bias, d.slope = _ptr(pack.scale), _ptr(pack.bias), _ptr(pack.slope)
-    d.act = ACT[act if act is not None else pack.act]
-    d.y_planes = int(y_planes)
-    check(lib().prpe_upconv_gemm(C.byref(d), _stream()), f"prpe_upconv_gemm[{pack.name}]")
     return y
 
 

@@ -303,3 +303,54 @@ def test_traffic_records_name_their_kernel_sources():
         h = bench.kernel_sources_hash(t["sources"])
         assert len(h) == 16 and h == bench.kernel_sources_hash(list(reversed(t["sources"])))
         assert h != bench.kernel_sources_hash(), "a subset hash must differ from the all-sources hash"
+
+
+def test_weight_versions_trigger_repack(monkeypatch):
+    """Host logic of the stale-weights guard (prpe/model.py ``_sync_weights``) without a GPU:
+    the engine is a stub counting repacks; in-place writes through the branch trees'
+    parameters, the trunk's ``parameters()`` and ``state_dict()`` values all mark the model stale."""
+    import torch
+    from prpe import arch, model as M, synth
+
+    built = []
+
+    class StubEngine:
+        def __init__(self, sd, device, precision):
+            built.append(1)
+
+    monkeypatch.setattr(M, "Engine", StubEngine)
+    sd = synth.make_state_dict(arch.state_dict_spec())
+    m = M.CombinedModel(sd, device="cuda")
+    assert len(built) == 1 and not m.weights_stale()
+    m._sync_weights()
+    assert len(built) == 1                                  # nothing changed: no repack
+    with torch.no_grad():
+        dict(m.vit_pose.adapter.named_parameters())["7.weight"].add_(1.0)
+    assert m.weights_stale()
+    m._sync_weights()
+    assert len(built) == 2 and not m.weights_stale()
+    with torch.no_grad():
+        next(iter(m.parameters())).mul_(2.0)                # a trunk parameter
+    assert m.weights_stale()
+    m._sync_weights()
+    with torch.no_grad():
+        m.state_dict()["yolo_face.adapter.0.weight"].zero_()
+    assert m.weights_stale()
+    m._sync_weights()
+    assert len(built) == 4 and not m.weights_stale()
+
+
+def test_every_environment_switch_is_documented():
+    """kernel routing must not depend on undocumented process-wide
+    environment variables -- every PRPE_* switch the library or the engine reads is listed in
+    INTEGRATION.md §4."""
+    import glob
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    pkg = os.path.join(root, "person-recognition-for-pose-estimation_amd")
+    read = set()
+    for f in glob.glob(os.path.join(pkg, "csrc", "*.hip")) + glob.glob(os.path.join(pkg, "prpe", "*.py")):
+        read |= set(re.findall(r'(?:getenv|environ\.get)\("(PRPE_[A-Z0-9_]+)"', open(f).read()))
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    documented = set(re.findall(r"PRPE_[A-Z0-9_]+", doc[doc.index("## 4. Environment switches"):]))
+    assert read and not (read - documented), sorted(read - documented)

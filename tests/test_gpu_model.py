@@ -107,9 +107,7 @@ def test_nms_on_model_output_bit_exact_vs_oracle(model, frames, golden_model):
     # discontinuous in its inputs, so report the fraction of reference detections that have a
     # same-class match (IoU >= 0.9, |score diff| < 1e-3) among ours (hard parts)
     ref = R.non_max_suppression(torch.from_numpy(golden_model["det_face_s8"]))
-    rates = [nms_match_rate(a.cpu(), b) for a, b in zip(ours, ref)]
-    print("end-to-end NMS detection match rate vs reference:", rates)
-    assert min(rates) == 1.0
+    assert_nms_end_to_end([a.cpu() for a in ours], ref)
 
 
 def _iou(a, b):
@@ -120,11 +118,77 @@ def _iou(a, b):
     return inter / (area(a)[:, None] + area(b)[None, :] - inter)
 
 
+def _matched(a, b):
+    """[len(a)] bool: row i of a has a same-class row in b with IoU >= 0.9 and |score diff| < 1e-3."""
+    if len(a) == 0 or len(b) == 0:
+        return torch.zeros(len(a), dtype=torch.bool)
+    ok = (_iou(a, b) >= 0.9) & ((a[:, None, 4] - b[None, :, 4]).abs() < 1e-3) & (a[:, None, 5] == b[None, :, 5])
+    return ok.any(1)
+
+
 def nms_match_rate(ours, ref):
     if len(ref) == 0:
         return 1.0 if len(ours) == 0 else 0.0
-    if len(ours) == 0:
-        return 0.0
-    iou = _iou(ref, ours)
-    ok = (iou >= 0.9) & ((ref[:, None, 4] - ours[None, :, 4]).abs() < 1e-3) & (ref[:, None, 5] == ours[None, :, 5])
-    return float(ok.any(1).float().mean())
+    return float(_matched(ref, ours).float().mean())
+
+
+def unexplained_nms_flips(ours, ref, iou_thr=0.65, conf_thr=0.001, eps=2e-3):
+    """Rows of either list without a match in the other that are NOT explained by a near-tie of
+    the greedy NMS (end to end, NMS runs on scores that differ from the oracle's by
+    ~3e-5, so a decision tied to that level may legitimately flip): a row is explained when its
+    score is within eps of the confidence threshold, or some row of either list overlaps it with
+    an IoU within eps of the IoU threshold (the suppression test IoU > thr can go either way)."""
+    out = []
+    both = torch.cat([ours, ref]) if len(ours) and len(ref) else (ours if len(ours) else ref)
+    for a, b in ((ours, ref), (ref, ours)):
+        miss = ~_matched(a, b)
+        for r in a[miss]:
+            near_conf = abs(float(r[4]) - conf_thr) < eps
+            iou = _iou(r[None], both)[0]
+            near_iou = bool(((iou - iou_thr).abs() < eps).any())
+            if not (near_conf or near_iou):
+                out.append(r.tolist())
+    return out
+
+
+def assert_nms_end_to_end(ours_list, ref_list, floor=0.98):
+    """End-to-end NMS agreement: every frame's match rate >= floor, and every mismatch a near-tie
+    (printed, so a flip is looked at rather than absorbed by the floor)."""
+    rates = [nms_match_rate(a, b) for a, b in zip(ours_list, ref_list)]
+    print("end-to-end NMS detection match rate vs reference:", rates)
+    for f, (a, b) in enumerate(zip(ours_list, ref_list)):
+        if rates[f] < 1.0 or len(a) != len(b):
+            bad = unexplained_nms_flips(a, b)
+            print(f"frame {f}: match rate {rates[f]:.4f}, {len(a)} vs {len(b)} rows, unexplained flips: {bad}")
+            assert not bad, (f, bad)
+    assert min(rates) >= floor, rates
+
+
+def test_inplace_weight_edit_is_never_stale(state_dict, frames):
+    """an in-place edit through ``parameters()`` (what an optimizer
+    step in pl.Trainer.fit does before validation, round_robin_trainer.py:258-262) must reach
+    the next forward. The edited model is checked against the oracle on its own state_dict."""
+    sd = {k: v.clone() for k, v in state_dict.items()}     # the session fixture stays unedited
+    m = CombinedModel(sd, device="cuda")
+    m.set_task("pose_estimation")
+    h0 = m(frames).heatmaps.cpu()
+    assert not m.weights_stale()
+    named = dict(m.vit_pose.adapter.named_parameters())
+    with torch.no_grad():
+        named["7.weight"].mul_(1.5)                        # the dominant conv (modify_models.py:366)
+        named["8.bias"].add_(0.25)                         # its BatchNorm (folded at pack time)
+    assert m.weights_stale()
+    h1 = m(frames).heatmaps.cpu()
+    assert not m.weights_stale()
+    ref = R.combined_forward(m.state_dict(), frames.cpu(), "pose_estimation")
+    assert float((h1 - h0).abs().max()) > 1e-2               # the edit changes the output ...
+    assert float((h1 - ref).abs().max()) <= 1e-3             # ... and the engine follows it
+    # the trunk through CombinedModel.parameters() and an edit through state_dict() values
+    p = next(iter(m.parameters()))
+    with torch.no_grad():
+        p.mul_(0.75)
+        m.state_dict()["vit_pose.adapter.11.bias"].add_(0.1)
+    assert m.weights_stale()
+    h2 = m(frames).heatmaps.cpu()
+    ref2 = R.combined_forward(m.state_dict(), frames.cpu(), "pose_estimation")
+    assert float((h2 - ref2).abs().max()) <= 1e-3

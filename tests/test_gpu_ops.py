@@ -1120,6 +1120,42 @@ def test_vit_attention_head_major_operand_bit_identical():
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B", [4, 1232])
+def test_vit_attention_frame_interleaved_operand(B):
+    """a frame-interleaved [L, B, 3, H, D] operand (s_tok = B * 3HD). At B = 4 the
+    frame's extent fits the whole-head kernel's 32-bit buffer offsets (bit-identical to the
+    row-major call); at B = 1232 it spans > 2^31 bytes and must be routed to the 64-bit streaming
+    kernel instead of silently reading zeros (checked against fp64 on spread frames)."""
+    L, H, D = 192, 12, 64
+    qkv = rnd(B * L, 3 * H * D, seed=46, scale=2.0).to(DEV)
+    a = torch.empty(B * L, H * D, device=DEV)
+    ops.attention(qkv, a, B, L, H, D, D ** -0.5)
+    il = qkv.view(B, L, 3 * H * D).transpose(0, 1).contiguous()          # [L, B, 3HD]
+    st = (3 * H * D, H * D, D, B * 3 * H * D)
+    assert ((L - 1) * st[3] + 2 * st[1] + (H - 1) * st[2] + D) * 4 >= (1 << 31) or B < 1000
+    b = torch.empty(B * L, H * D, device=DEV)
+    ops.attention_strided(il, st, b, B, L, H, D, D ** -0.5)
+    torch.cuda.synchronize()
+    if B < 1000:
+        assert torch.equal(a, b)
+        return
+    del il
+    ac, bc = a.cpu(), b.cpu()
+    for f in (0, B // 2, B - 1):
+        q, k, v = qkv[f * L:(f + 1) * L].cpu().view(L, 3, H, D).permute(1, 2, 0, 3).double()
+        ref = (torch.softmax(q @ k.transpose(-1, -2) * D ** -0.5, -1) @ v).transpose(0, 1).reshape(L, H * D)
+        torch.testing.assert_close(bc[f * L:(f + 1) * L], ref.float(), rtol=0, atol=5e-5)
+    torch.testing.assert_close(bc, ac, rtol=0, atol=1e-4)    # two kernels, each within 5e-5 of fp64
+
+
+def test_vit_attention_negative_stride_rejected():
+    B, L, H, D = 2, 192, 12, 64
+    qkv = rnd(B * L, 3 * H * D, seed=47).to(DEV)
+    out = torch.empty(B * L, H * D, device=DEV)
+    with pytest.raises(PrpeError):
+        ops.attention_strided(qkv, (L * 3 * H * D, H * D, D, -3 * H * D), out, B, L, H, D, D ** -0.5)
+
+
 @pytest.mark.parametrize("hw", [5, 20, 17])
 def test_psa_attention(hw):
     """5x5: the LDS score-matrix kernel (the model's P5 after the adapter); 20x20 (raw 640x640
@@ -1211,54 +1247,3 @@ def test_copy_pad_nchw_to_padded_nhwc(yc, flip):
     assert torch.equal(ya.cpu(), frame_amax(x))                # per-frame max|y|
     # the border is untouched
     assert torch.equal(buf[:, :3].cpu(), torch.full_like(buf[:, :3].cpu(), 7.0))
-
-
-@pytest.mark.parametrize("N,hi,wi,ho,wo,ac,C", [(2, 20, 20, 160, 160, True, 512), (1, 10, 12, 64, 70, True, 64),
-                                              (2, 13, 9, 70, 53, False, 96), (1, 20, 20, 160, 160, False, 32)])
-def test_upconv_gemm_bit_exact_vs_unfused(N, hi, wi, ho, wo, ac, C):
-    """prpe_upconv_gemm (the face-YOLO adapter's .4 upconv + BN + SiLU and .7 1x1 + BN + SiLU in one
-    launch) == prpe_upconv3x3 (planes output) followed by prpe_conv2d (precision 0, planes input,
-    planes output) bit for bit: the same interpolation / BN / SiLU / split arithmetic and the same
-    GEMM K order. Model shape (20 -> 160, 512 -> 256) and ragged ones (partial 16-pixel tiles, both
-    align_corners modes, other channel counts)."""
-    Co = 256
-    z = rnd(N, hi, wi, 9 * C, seed=510, scale=0.5).to(DEV)
-    us = (torch.rand(C, generator=_g(511)) + 0.5).to(DEV)
-    ub = rnd(C, seed=512).to(DEV)
-    w = rnd(Co, C, 1, 1, seed=513, scale=1.0 / math.sqrt(C))
-    sc = torch.rand(Co, generator=_g(514)) + 0.5
-    bi = rnd(Co, seed=515)
-    pk = pack.pack_conv("ug", w, 1, 0, DEV, scale=sc, bias=bi, act="silu")
-    u = torch.empty(N, ho, wo, C, device=DEV)
-    ops.upconv3x3(z, u, ac, us, ub, None, "silu", y_planes=True)
-    ref = torch.empty(N, ho, wo, Co, device=DEV)
-    ops.conv2d(u, pk, ref, precision=0, x_planes=True, y_planes=True)
-    got = torch.empty(N, ho, wo, Co, device=DEV)
-    ops.upconv_gemm(z, pk, got, ac, us, ub, up_act="silu", y_planes=True)
-    torch.cuda.synchronize()
-    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
-    # and the fp32 form of the output equals the unfused fp32 GEMM
-    ref32 = torch.empty(N, ho, wo, Co, device=DEV)
-    ops.conv2d(u, pk, ref32, precision=0, x_planes=True)
-    got32 = torch.empty(N, ho, wo, Co, device=DEV)
-    ops.upconv_gemm(z, pk, got32, ac, us, ub, up_act="silu")
-    torch.cuda.synchronize()
-    assert torch.equal(got32, ref32)
-
-
-def test_upconv_gemm_rejects():
-    """A source window over 5 rows per 16-pixel tile (upsampling ratio < ~4), Co != 256 and a
-    K-mismatched pack are refused (-EINVAL / ValueError), nothing is launched."""
-    z = torch.zeros(1, 20, 20, 9 * 64, device=DEV)
-    pk = pack.pack_conv("ug", rnd(256, 64, 1, 1, seed=520), 1, 0, DEV)
-    with pytest.raises(PrpeError):
-        ops.upconv_gemm(z, pk, torch.empty(1, 40, 40, 256, device=DEV), True, torch.ones(64, device=DEV),
-                        torch.zeros(64, device=DEV))
-    pk128 = pack.pack_conv("ug", rnd(128, 64, 1, 1, seed=521), 1, 0, DEV)
-    with pytest.raises(PrpeError):
-        ops.upconv_gemm(z, pk128, torch.empty(1, 160, 160, 128, device=DEV), True, torch.ones(64, device=DEV),
-                        torch.zeros(64, device=DEV))
-    pk32 = pack.pack_conv("ug", rnd(256, 32, 1, 1, seed=522), 1, 0, DEV)
-    with pytest.raises(ValueError):
-        ops.upconv_gemm(z, pk32, torch.empty(1, 160, 160, 256, device=DEV), True, torch.ones(64, device=DEV),
-                        torch.zeros(64, device=DEV))

@@ -20,6 +20,7 @@ hipcc."""
 import concurrent.futures as cf
 import glob
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -130,9 +131,14 @@ def test_checker_flags_store_data_overwritten_by_the_next_instruction():
 \ts_endpgm
 """
     assert len(_kernel(body).store_data_overwrites()) == 1
-    # one wait state (s_nop 0) or an unrelated instruction in between: clear
-    assert _kernel(body.replace("\tv_pk", "\ts_nop 0\n\tv_pk")).store_data_overwrites() == []
-    assert _kernel(body.replace("\tv_pk", "\tv_add_u32_e32 v1, 4, v2\n\tv_pk")).store_data_overwrites() == []
+    # one wait state (s_nop 0, or one unrelated instruction) is not enough: still flagged
+    assert len(_kernel(body.replace("\tv_pk", "\ts_nop 0\n\tv_pk")).store_data_overwrites()) == 1
+    assert len(_kernel(body.replace("\tv_pk", "\tv_add_u32_e32 v1, 4, v2\n\tv_pk")).store_data_overwrites()) == 1
+    # two wait states (s_nop 1, the GPU-verified fix, or two unrelated instructions): clear
+    assert _kernel(body.replace("\tv_pk", "\ts_nop 1\n\tv_pk")).store_data_overwrites() == []
+    assert _kernel(body.replace("\tv_pk", "\tv_add_u32_e32 v1, 4, v2\n\ts_nop 0\n\tv_pk")).store_data_overwrites() == []
+    assert _kernel(body.replace("\tv_pk", "\tv_add_u32_e32 v1, 4, v2\n\tv_add_u32_e32 v3, 4, v2\n\tv_pk"))\
+        .store_data_overwrites() == []
     # 64-bit stores, and writes of other registers, are not flagged
     assert _kernel(body.replace("dwordx4 v[36:39]", "dwordx2 v[36:37]")).store_data_overwrites() == []
     assert _kernel(body.replace("v_pk_mul_f32 v[36:37]", "v_pk_mul_f32 v[40:41]")).store_data_overwrites() == []
@@ -195,10 +201,22 @@ def test_occupancy_critical_tiles_fit_128_vgprs_without_spills(asm_dir):
     # two-K-step tile (AdaFace) run two / four workgroups per CU only at <= 128 VGPRs; round 5's
     # GELU rewrite silently pushed them to 132 (one / three per CU: trunk convs 15-27 % slower).
     # Their launch bound now asks for 4 waves per SIMD; this pins that it costs no spills.
+    #  every instantiation that conv_wave.hip's wave_wps maps to 4 waves per SIMD is
+    # checked, not only the two measured ones: NW 8, TM 2, NP 2 without prologue (bf16, f16, dual,
+    # planes-input variants alike) and NW 4, TM 2, single-plane (ONE) with KSF 1, no prologue
     meta = _kernel_meta([o for o in asm_dir if o.endswith("conv_wave.s")][0])
-    hot = {k: v for k, v in meta.items()
-           if "conv_wave_kernelILi8ELi2ELi8ELi2ELi3ELb0ELb1E" in k        # NW 8, TM 2, TN 8, p3, no prologue
-           or "conv_wave_kernelILi4ELi2ELi8ELi2ELi2ELb0ELb1ELb0ELb0ELb1ELi1E" in k}   # p4, KSF 1
-    assert len(hot) >= 3, sorted(meta)
+
+    def targs(name):   # NW, TM, TN, NP, STAGES, PRO, F16, DUAL, APL, ONE, KSF from the mangled name
+        m = re.search(r"conv_wave_kernelI((?:L[ib]n?\d+E)+)E", name)
+        return [int(v.replace("n", "-")) for v in re.findall(r"L[ib](n?\d+)E", m.group(1))] if m else None
+
+    def wps4(a):
+        nw, tm, _tn, np_, _st, pro, _f16, _dual, _apl, one, ksf = a
+        return (nw == 8 and tm == 2 and np_ == 2 and not pro) or (nw == 4 and tm == 2 and one and ksf == 1 and not pro)
+
+    hot = {k: v for k, v in meta.items() if targs(k) and len(targs(k)) == 11 and wps4(targs(k))}
+    assert any("conv_wave_kernelILi8ELi2ELi8ELi2ELi3ELb0ELb1E" in k for k in hot), sorted(meta)   # p3 256x128
+    assert any("conv_wave_kernelILi4ELi2ELi8ELi2ELi2ELb0ELb1ELb0ELb0ELb1ELi1E" in k for k in hot)   # p4, KSF 1
+    assert len(hot) >= 4, sorted(hot)
     for k, (v, spill) in hot.items():
         assert v <= 128 and spill == 0, (k, v, spill)

@@ -53,7 +53,10 @@ BRANCH = re.compile(r"^s_(c)?branch\w*\s+(\.LBB\w+)")
 STORE_PREFIX = ("ds_write", "ds_store", "buffer_store", "global_store", "scratch_store", "flat_store")
 VMEM_PREFIX = ("buffer_", "global_", "scratch_", "flat_", "tbuffer_")
 VMEM_NOT_COUNTED = ("buffer_inv", "buffer_wbl2", "buffer_wbinvl1", "buffer_gl")
-STORE_DATA_STATES = 1                  # wait states a >64-bit store's data VGPRs must stay unwritten
+# wait states a >64-bit store's data VGPRs must stay unwritten: 2, the fix verified on the GPU
+# (``s_nop 1`` after each store, tools/bneck_8308_nop.py) and LLVM's gfx940+ VMEM-store-data
+# hazard model (2 VALU wait states); one state is unverified and not taken as safe
+STORE_DATA_STATES = 2
 
 
 def regs(txt):
@@ -194,7 +197,10 @@ class Kernel:
     def hoisted_reads(self):
         bad = []
         for it in self.insts:
-            if not it.is_lds_read:
+            # LDS reads written as inline asm are placed by the source, not by the scheduler (a
+            # volatile asm keeps its order against the barrier asm): they cannot be hoisted, and
+            # their results may legitimately live across later barriers (the upconv's H rows)
+            if not it.is_lds_read or it.asm:
                 continue
             dst = it.dst()
             if not dst:

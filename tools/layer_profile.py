@@ -33,7 +33,10 @@ def main():
     # fused bottlenecks (Engine.bottleneck) are timed under the block name; their row shows conv2
     e.watch |= {f"backbone.layer{li}.{b}" for li, (_, n, _) in enumerate(arch.RESNET50_STAGES, 1)
                 for b in range(n)}
+    # the bilinear-upsample -> 3x3 rewrites' second stage (prpe_upconv3x3), by adapter
+    e.watch |= {k.rsplit(":", 1)[0] + ":upconv" for k in e._packs if k.endswith(":taps")}
     e.events = {}
+    e.up_events = {}
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     t0.record()
@@ -61,6 +64,18 @@ def main():
             comp = "ada_face"
         by[comp] = by.get(comp, 0.0) + ms
     print("by component:", {k: round(v, 2) for k, v in sorted(by.items(), key=lambda t: -t[1])})
+    # upconvs: time, and the rate of their output writes (the bound: z reads are small and L2-hot)
+    up = []
+    for name, evs in e.up_events.items():
+        ms = sum(s.elapsed_time(f) for s, f, *_ in evs)
+        yb = sum(ev[2] for ev in evs)
+        zb = sum(ev[3] for ev in evs)
+        up.append((ms, name, len(evs), yb, zb, evs[0][4], evs[0][5]))
+    up.sort(reverse=True)
+    print(f"upconvs (prpe_upconv3x3): {sum(u[0] for u in up):.3f} ms in total")
+    for ms, name, n, yb, zb, pl, act in up:
+        print(f"{ms:8.3f}  y {yb / 1e9:6.2f} GB -> {yb / ms / 1e9:6.2f} TB/s of writes  (z {zb / 1e9:5.2f} GB)  "
+              f"{'planes' if pl else 'fp32'} {act:5s} {name} x{n}")
 
 
 if __name__ == "__main__":

@@ -4,6 +4,7 @@ prpe._lib loads it on the box in place of libprpe.so; tools/bneck_ablate.sh-styl
 
     python tools/rev_variant_build.py REV csrc/conv_bneck.hip TAG   # -> tools/abl/libprpe_TAG.so
     python tools/rev_variant_build.py WORK csrc/conv_halo.hip TAG --patch OLD NEW [--patch ...]
+    python tools/rev_variant_build.py /tmp/variant.hip csrc/pointwise.hip TAG   # a scratch copy
         (WORK = the working tree's file; measurement variants; csrc files may be comma-separated)
 
 Run after person-recognition-for-pose-estimation_amd/build.py (it reuses build/*.o).
@@ -36,6 +37,8 @@ def main():
         name = os.path.basename(rel)
         if rev == "WORK":
             src = open(os.path.join(PKG, rel)).read()
+        elif os.path.isfile(rev):                 # a scratch copy of the file (one csrc file)
+            src = open(rev).read()
         else:
             src = subprocess.run(["git", "-C", ROOT, "show", f"{rev}:person-recognition-for-pose-estimation_amd/{rel}"],
                                  capture_output=True, text=True, check=True).stdout
