@@ -480,6 +480,134 @@ __global__ __launch_bounds__(256) void upconv_dma_kernel(UpK p, int R, int rbloc
   if (p.y_amax) amax_commit(p.y_amax + n, ym);
 }
 
+// Unit-scale form (round 6): the Co <= 4 tap rewrites (Engine.conv3x3_smallco: ViTPose adapter.10
+// 128 -> 3, face-YOLO adapter.16 64 -> 3) run prpe_upconv3x3 with the output grid = the input grid
+// and align_corners, where every interpolation weight is 0 and every source index exact: the
+// "upconv" is the plain 3x3 tap sum
+//   y[n, oy, ox, c] = EPI( sum_dy sum_dx z[n, oy+dy-1, ox+dx-1, (3 dy + dx) Co + c] )
+// over the taps inside the image. The rolling-row kernel took 0.86 ms for the ViT one (1.36 GB of z
+// at bs = 256, 1.6 TB/s: one thread per channel); a thread per pixel gathering its nine Co-float
+// slices took 1.01 ms (each dword load of a wave touched 64 cache lines at the 9 Co-float pixel
+// pitch; profiles/r06_layer_profile_unit_gather.txt). Here one wave walks a 64-pixel column strip
+// down a chunk of R output rows: each z row's segment (66 pixels x 9 Co floats, contiguous) is read
+// with lane-contiguous dword loads (two cache lines per instruction), one row ahead in registers,
+// staged through the wave's LDS slice, and every lane takes the 27 values its pixel needs (the
+// three dy slices of the row feed three output rows in flight). Sums in the rolling-row kernel's
+// order (per dy its dx taps, then the dy rows, each step an IEEE add), the same epilogue
+// expression: the same bits for finite z (the general form adds 0 * (the next column), so a
+// non-finite z one column outside a tap's support made its sum NaN; here it does not). A block
+// (4 waves) is one frame: the per-frame max|y| slot.
+constexpr int UPU_R = 32;                               // output rows per chunk
+template <int CO>
+__global__ __launch_bounds__(256) void upconv_unit_kernel(UpK p, int nstrip, int ngroups, int rchunks) {
+  constexpr int ZP = 9 * CO;                            // floats per z pixel
+  constexpr int SEG = 66 * ZP;                          // one row segment: pixels x0 - 1 .. x0 + 64
+  constexpr int NL = (SEG + 63) / 64;                   // dword loads per lane and row
+  __shared__ float seg_all[4][NL * 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int t = blockIdx.x;
+  const int sg = t % ngroups;
+  t /= ngroups;
+  const int rc = t % rchunks;
+  const int n = t / rchunks;
+  const int H = p.y.h, W = p.y.w;
+  const int strip = sg * 4 + wave;
+  float ym = 0.f;
+  if (strip < nstrip) {
+    float* seg = seg_all[wave];
+    const int x0 = strip * 64, x = x0 + lane;
+    const bool live = x < W;
+    const int oy0 = rc * UPU_R, oy1 = oy0 + UPU_R < H ? oy0 + UPU_R : H;
+    const int r0 = oy0 > 0 ? oy0 - 1 : 0, r1 = oy1 < H ? oy1 : H - 1;
+    const float* zn = p.z.ptr + (int64_t)n * p.z.sn;
+    // this lane's loads of a row: segment index j = lane + 64 k -> z pixel x0 - 1 + j / ZP
+    int jo[NL];
+    bool jv[NL];
+#pragma unroll
+    for (int k = 0; k < NL; ++k) {
+      const int j = lane + 64 * k;
+      const int px = x0 - 1 + j / ZP;
+      jv[k] = j < SEG && px >= 0 && px < W;
+      jo[k] = (x0 - 1) * ZP + j;                        // float offset inside the z row
+    }
+    float nxt[NL];
+    auto load_row = [&](int r) {
+      const float* zr = zn + (int64_t)r * p.z.sh;
+#pragma unroll
+      for (int k = 0; k < NL; ++k) nxt[k] = jv[k] ? zr[jo[k]] : 0.f;
+    };
+    float scv[CO], biv[CO], slv[CO];
+#pragma unroll
+    for (int c = 0; c < CO; ++c) {
+      scv[c] = p.scale ? p.scale[c] : 1.f;
+      biv[c] = p.bias ? p.bias[c] : 0.f;
+      slv[c] = p.slope ? p.slope[c] : 0.f;
+    }
+    auto add = [](float a, float b) {
+      float r;
+      asm("v_add_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+      return r;
+    };
+    auto store = [&](int o, const float (&acc)[CO]) {
+      if (!live) return;
+      float* y = p.y.ptr + (int64_t)n * p.y.sn + (int64_t)o * p.y.sh + (int64_t)x * p.y.sw;
+#pragma unroll
+      for (int c = 0; c < CO; ++c) {
+        const float out = apply_act(acc[c] * scv[c] + biv[c], p.act, slv[c]);
+        ym = fmaxf(ym, fabsf(out));
+        y[(int64_t)c * p.y.sc] = out;
+      }
+    };
+    float accA[CO], accB[CO];                           // outputs r - 1 and r
+#pragma unroll
+    for (int c = 0; c < CO; ++c) accA[c] = accB[c] = 0.f;
+    load_row(r0);
+    for (int r = r0; r <= r1; ++r) {
+      // the row into the wave's LDS slice (every lane's previous reads retired first), then the
+      // next row's loads in flight while this one is summed
+      __builtin_amdgcn_s_waitcnt(0xc07f);              // lgkmcnt(0): last row's ds_reads done
+#pragma unroll
+      for (int k = 0; k < NL; ++k) seg[lane + 64 * k] = nxt[k];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      if (r < r1) load_row(r + 1);
+      float h[3][CO];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+#pragma unroll
+        for (int c = 0; c < CO; ++c) h[dy][c] = 0.f;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {
+          const int xx = x + dx - 1;
+          if ((unsigned)xx >= (unsigned)W) continue;
+          const float* sp = seg + (lane + dx) * ZP + (dy * 3 + dx) * CO;
+#pragma unroll
+          for (int c = 0; c < CO; ++c) h[dy][c] = add(h[dy][c], sp[c]);
+        }
+      }
+      // dy = 2 -> output r - 1 (complete), dy = 1 -> output r, dy = 0 -> output r + 1 (first term)
+      if (r >= 1) {
+#pragma unroll
+        for (int c = 0; c < CO; ++c) accA[c] = add(accA[c], h[2][c]);
+        if (r - 1 >= oy0) store(r - 1, accA);
+      }
+      float accC[CO];
+#pragma unroll
+      for (int c = 0; c < CO; ++c) {
+        accB[c] = add(accB[c], h[1][c]);
+        accC[c] = add(0.f, h[0][c]);
+      }
+#pragma unroll
+      for (int c = 0; c < CO; ++c) {
+        accA[c] = accB[c];
+        accB[c] = accC[c];
+      }
+    }
+    if (oy1 == H) store(H - 1, accA);                   // the last row has no dy = 2 term
+  }
+  if (p.y_amax) amax_commit(p.y_amax + n, ym);
+}
+
 // Separable form of the same sum (6 loads per output instead of 36):
 //   H[n][dy][r][ox][c] = sum_dx valid(ox+dx-1) * lerp_x(Z_{dy,dx}[n, r, :, c], sx(ox+dx-1))
 //   y[n][oy][ox][c]    = EPI( sum_dy valid(oy+dy-1) * lerp_y(H[n][dy][:, ox, c], sy(oy+dy-1)) )
@@ -1009,6 +1137,22 @@ extern "C" int prpe_upconv3x3(const prpe_view* z, const prpe_view* y, int32_t al
     } else {
       hipLaunchKernelGGL(upconv_h_kernel<1>, g_h, dim3(256), 0, st, p, H);
       hipLaunchKernelGGL(upconv_out_kernel<1>, g_out, dim3(256), 0, st, p, (const float*)H);
+    }
+    return launch_status();
+  }
+  // unit scale (output grid = input grid, align_corners: every weight 0) with Co <= 4: the tap sum
+  // (upconv_unit_kernel, same bits for finite z)
+  if (align_corners && y->c <= 4 && z->h == y->h && z->w == y->w && !y_planes && z->sc == 1 &&
+      z->sw == z->c && z->sh >= 0 && z->sn >= 0 && y->sh >= 0 && y->sw >= 0 && y->sc >= 0) {
+    const int nstrip = (y->w + 63) / 64, ngroups = (nstrip + 3) / 4, rchunks = (y->h + UPU_R - 1) / UPU_R;
+    const int64_t nb = (int64_t)y->n * rchunks * ngroups;
+    if (nb >= (1LL << 31)) return PRPE_EINVAL;
+    const dim3 g((unsigned)nb), b(256);
+    switch (y->c) {
+      case 1: hipLaunchKernelGGL(upconv_unit_kernel<1>, g, b, 0, st, p, nstrip, ngroups, rchunks); break;
+      case 2: hipLaunchKernelGGL(upconv_unit_kernel<2>, g, b, 0, st, p, nstrip, ngroups, rchunks); break;
+      case 3: hipLaunchKernelGGL(upconv_unit_kernel<3>, g, b, 0, st, p, nstrip, ngroups, rchunks); break;
+      default: hipLaunchKernelGGL(upconv_unit_kernel<4>, g, b, 0, st, p, nstrip, ngroups, rchunks); break;
     }
     return launch_status();
   }

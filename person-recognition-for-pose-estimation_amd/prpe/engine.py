@@ -83,6 +83,10 @@ BNECK_L2 = os.environ.get("PRPE_BNECK_L2", "1") != "0"
 # stem conv + max-pool as ONE launch (prpe_stem_maxpool: the [B, 320, 320, 64] stem map stays in
 # LDS); PRPE_STEM_POOL=0 runs prpe_conv2d + prpe_maxpool
 STEM_POOL = os.environ.get("PRPE_STEM_POOL", "1") != "0"
+# ViTPose patch embedding (16x16/16 pad 2, 3 -> 768) as a chunked 16x1 conv over an overlapping view
+# of a zero-bordered NHWC4 copy of the crops, as the stem (Engine.vit_pix4); PRPE_VIT_PATCH_VIEW=0
+# runs the plain 16x16 conv on the 3-channel crops (the gather-bound small-Ci kernel)
+PATCH_VIEW = os.environ.get("PRPE_VIT_PATCH_VIEW", "1") != "0"
 
 
 class _Prec:
@@ -315,7 +319,7 @@ class Engine:
             out._prpe_planes = True
         return out
 
-    def conv3x3_smallco(self, x, name, wkey, bn=None, bias_key=None, act="none"):
+    def conv3x3_smallco(self, x, name, wkey, bn=None, bias_key=None, act="none", out=None):
         """3x3 stride-1 pad-1 conv + BN + act for Co <= 4. The direct implicit GEMM re-reads
         the input once per tap for 3 useful output columns; here z = x W_taps (1x1, 9*Co
         outputs, the input read once) and y = act(BN(sum_tap shift_tap(z_tap))) by the tap
@@ -323,8 +327,9 @@ class Engine:
         unit scale: every source index is exact, interpolation weights 1 and 0). Same
         function as the conv; fp32 summation order differs."""
         if SMALLCO_TAPS:
-            return self.upconv(name, x, wkey, (x.shape[1], x.shape[2]), True, bn=bn, bias_key=bias_key, act=act)
-        return self.conv(x, self.pk(name, wkey, 1, 1, bn=bn, bias_key=bias_key, act=act))
+            return self.upconv(name, x, wkey, (x.shape[1], x.shape[2]), True, bn=bn, bias_key=bias_key, act=act,
+                               out=out)
+        return self.conv(x, self.pk(name, wkey, 1, 1, bn=bn, bias_key=bias_key, act=act), out=out)
 
     # ------------------------------------------------------------------ ResNet-50 trunk
     def trunk(self, x_nchw, flip_w=False):
@@ -699,11 +704,35 @@ class Engine:
             z = self.empty(B, H, W, w2.shape[0])
             sink = self.dev("sink:" + str(p7.co), lambda: torch.zeros(p7.co)).expand(B, H, W, p7.co)
             self.conv(u, p7, out=sink, w2=w2, y2=z)
+            out = self._vit_pix_out(B)
             return self.upconv(a + ".10", None, a + ".10.weight", (H, W), True, bn=a + ".11",
-                               bias_key=a + ".10.bias", act="gelu", z=z)
+                               bias_key=a + ".10.bias", act="gelu", z=z, out=out)
         t = self.conv(u, p7)
         return self.conv3x3_smallco(t, a + ".10", a + ".10.weight", bn=a + ".11", bias_key=a + ".10.bias",
-                                    act="gelu")
+                                    act="gelu", out=self._vit_pix_out(t.shape[0]))
+
+    # ---- the ViTPose crops in a zero-bordered NHWC4 buffer [B, 256+4, 192+4, 4] (2 rows / columns
+    # of padding = the patch conv's pad, the 4th channel 0): the adapter's last conv writes the
+    # interior, the patch embedding reads the overlapping view of vit_pix4 (as the stem's buffer)
+    def vit_pix4(self, B):
+        H, W = arch.VIT_IMG
+        key = ("vit_pix4", B)
+        buf = self._aux.get(key)
+        if buf is None:
+            for k in [k for k in self._aux if isinstance(k, tuple) and k[0] == "vit_pix4"]:
+                del self._aux[k]                       # one batch size at a time
+            buf = torch.zeros(B, H + 4, W + 4, 4, device=self.device, dtype=torch.float32)
+            self._aux[key] = buf
+        return buf
+
+    def _vit_pix_out(self, B):
+        if not PATCH_VIEW:
+            return None
+        H, W = arch.VIT_IMG
+        buf = self.vit_pix4(B)
+        out = buf[:, 2:2 + H, 2:2 + W, :3]
+        out._prpe_pix4 = buf
+        return out
 
     def _lin(self, name, wkey, bkey, act="none"):
         p = self._packs.get(name)
@@ -720,13 +749,35 @@ class Engine:
         B = pix.shape[0]
         Hp, Wp = arch.VIT_GRID
         L, D = Hp * Wp, arch.VIT_HIDDEN
-        patch = self.pk("vit.patch", v + ".embeddings.patch_embeddings.projection.weight", 16, 2,
-                        bias_key=v + ".embeddings.patch_embeddings.projection.bias")
         pos = self.dev("vit.possum", lambda: (self.sd[v + ".embeddings.position_embeddings"][0, 1:] +
                                               self.sd[v + ".embeddings.position_embeddings"][0, :1]))
         X = self.empty(B, Hp, Wp, D)
         pos_v = pos.view(1, Hp, Wp, D).expand(B, Hp, Wp, D)
-        self.conv(pix, patch, out=X, res=pos_v, res_mode=RES_PRE)
+        if PATCH_VIEW:
+            # the 16x16/16 pad-2 patch conv over 3 channels as a 16x1/16 conv over 64-"channel" pixels:
+            # V[b, h, w, 0:64] = P4[b, h, w : w+16, 0:4] (pixel stride 4 floats), P4 the zero-bordered
+            # NHWC4 crops (the padding is the conv's); W'[co][kw*4 + c][kh] = W[co, c, kh, kw] (0 for
+            # c = 3). One contiguous 256-B row segment per tap row: the chunked implicit GEMM
+            P4 = getattr(pix, "_prpe_pix4", None)
+            if P4 is None:                             # pixel_values from the caller (config 3)
+                P4 = self.vit_pix4(B)
+                ops.copy_pad(pix, P4[:, 2:2 + pix.shape[1], 2:2 + pix.shape[2], :])
+            Hv, Wv = P4.shape[1], (Wp - 1) * arch.VIT_PATCH + 1
+            V = P4.as_strided((B, Hv, Wv, 64), (P4.stride(0), P4.stride(1), 4, 1))
+            patch = self._packs.get("vit.patch4")
+            if patch is None:
+                w = self.sd[v + ".embeddings.patch_embeddings.projection.weight"].float()    # [768, 3, 16, 16]
+                wv = torch.zeros(w.shape[0], 16, 16, 4)
+                wv[..., :3] = w.permute(0, 2, 3, 1)                                        # [co, kh, kw, c]
+                w4 = wv.permute(0, 2, 3, 1).reshape(w.shape[0], 64, 16, 1)                # [co, kw*4 + c, kh, 1]
+                patch = pack_conv("vit.patch4", w4, 16, 0, self.device,
+                                  bias=self.sd[v + ".embeddings.patch_embeddings.projection.bias"])
+                self._packs["vit.patch4"] = patch
+            self.conv(V, patch, out=X, res=pos_v, res_mode=RES_PRE)
+        else:
+            patch = self.pk("vit.patch", v + ".embeddings.patch_embeddings.projection.weight", 16, 2,
+                            bias_key=v + ".embeddings.patch_embeddings.projection.bias")
+            self.conv(pix, patch, out=X, res=pos_v, res_mode=RES_PRE)
         X2 = X.view(B * L, D)
         as4 = lambda t: t.view(t.shape[0], 1, 1, t.shape[1])
 

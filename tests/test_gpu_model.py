@@ -192,3 +192,21 @@ def test_inplace_weight_edit_is_never_stale(state_dict, frames):
     h2 = m(frames).heatmaps.cpu()
     ref2 = R.combined_forward(m.state_dict(), frames.cpu(), "pose_estimation")
     assert float((h2 - ref2).abs().max()) <= 1e-3
+
+
+def test_vit_patch_embedding_view_matches_plain_conv(model, frames, monkeypatch):
+    """Round 6: the ViTPose patch embedding runs as a 16x1/16 conv over the overlapping view of the
+    zero-bordered NHWC4 crops (Engine.vit_pix4, written in place by the adapter's last conv, or by
+    copy_pad from caller pixel_values). Same function as the 16x16/16 pad-2 conv on the 3-channel
+    crops (PRPE_VIT_PATCH_VIEW=0): different K order, so within fp32 rounding, not bit-identical;
+    both through the model (adapter path) and from pixel values (config 3)."""
+    from prpe import engine as E
+    model.set_task("pose_estimation")
+    h_view = model(frames).heatmaps.cpu()
+    pix = synth.uniform(7, "pixel_values:2x256x192", (2, 3, 256, 192)).cuda()
+    p_view = model.vitpose_from_pixels(pix).heatmaps.cpu()
+    monkeypatch.setattr(E, "PATCH_VIEW", False)
+    h_plain = model(frames).heatmaps.cpu()
+    p_plain = model.vitpose_from_pixels(pix).heatmaps.cpu()
+    assert float((h_view - h_plain).abs().max()) <= 5e-5
+    assert float((p_view - p_plain).abs().max()) <= 5e-5

@@ -879,6 +879,31 @@ def test_conv3x3_smallco_tap_rewrite(h, w, ci, co, act):
     torch.testing.assert_close(y.permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=2e-4)
 
 
+@pytest.mark.parametrize("co", [1, 3, 4])
+@pytest.mark.parametrize("act", ["gelu", "silu", "prelu"])
+def test_upconv_unit_scale_tap_sum_bit_exact(co, act):
+    """The unit-scale upconv (output grid = input grid, align_corners; round 6's tap-sum kernel for
+    Co <= 4) == the two-pass separable form bit for bit, incl. an NHWC4-strided output view (the
+    4th channel untouched), and its per-frame max|y| slots."""
+    h, w = 37, 53
+    z = rnd(2, h, w, 9 * co, seed=240, scale=2.0).to(DEV)
+    sc = (torch.rand(co, generator=_g(241)) + 0.5).to(DEV)
+    bi = rnd(co, seed=242).to(DEV)
+    sl = (torch.rand(co, generator=_g(243)) * 0.3).to(DEV) if act == "prelu" else None
+    ref = torch.empty(2, h, w, co, device=DEV)
+    ops.upconv3x3(z, ref, True, sc, bi, sl, act, separable=True)
+    y = torch.empty(2, h, w, co, device=DEV)
+    ya = torch.zeros(2, device=DEV)
+    ops.upconv3x3(z, y, True, sc, bi, sl, act, y_amax=ya)
+    buf = torch.full((2, h, w, 4), 7.0, device=DEV)
+    ops.upconv3x3(z, buf[..., :co], True, sc, bi, sl, act)
+    torch.cuda.synchronize()
+    assert torch.equal(y.cpu(), ref.cpu())
+    assert torch.equal(buf[..., :co].cpu(), ref.cpu())
+    assert torch.equal(buf[..., co:].cpu(), torch.full_like(buf[..., co:].cpu(), 7.0))
+    assert torch.equal(ya.cpu(), ref.abs().amax(dim=(1, 2, 3)).cpu())
+
+
 @pytest.mark.parametrize("act", ["silu", "sigmoid", "gelu", "relu"])
 def test_epilogue_activation_accuracy(act):
     """apply_act (every conv / upconv epilogue; SiLU and sigmoid on the hardware exp2 with a
