@@ -44,6 +44,7 @@ SHAPES = {
     "ir50 body 3x3 128->128 @28": (28, 28, 128, 128, 3, 1, 1),
     "ir50 body 3x3 512->512 @7": (7, 7, 512, 512, 3, 1, 1),
     "trunk l2 conv3 1x1 128->512 +res @80": (80, 80, 128, 512, 1, 1, 0, "res"),
+    "trunk l3 conv3 1x1 256->1024 +res @40": (40, 40, 256, 1024, 1, 1, 0, "res"),
 }
 
 
