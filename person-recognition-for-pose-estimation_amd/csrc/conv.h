@@ -173,6 +173,15 @@ __device__ __forceinline__ void wait_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// a workgroup barrier for LDS traffic only: this wave's LDS writes done, then s_barrier.
+// __syncthreads() also fences global memory, i.e. waits vmcnt(0), draining every load, store
+// and LDS-DMA in flight (the in-order counter) where only LDS ordering is needed.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 // direct global->LDS kernel (conv_glds.hip): Ci % 32 == 0 channel-contiguous input, chunk-major
 // weights, precision 0 or 2, no prologue; tile 0 = auto, 10..12 = 256x128 / 256x64 / 128x128.
 // Returns PRPE_EINVAL when the shape is not eligible.

@@ -79,6 +79,9 @@ template <int MIDT, bool PROJ, int TRT = 8> struct BShape {
   static constexpr int CHB2 = TR * TC * 128;              // ... of t2
   static constexpr int CIN = PROJ ? MID : CIO;           // x channels
   static constexpr int NK1 = CIN / BK_;                  // phase-1 K-steps
+  // phase-1 A (x) lookahead in K-steps, in registers: 2 where four waves per SIMD cap VGPRs at
+  // 128 (inner width 64), 4 at one 8-wave workgroup per CU (inner width 128, 16 K-steps)
+  static constexpr int AD = MIDT > 64 ? 4 : 2;
   static constexpr int NKS3 = PROJ ? 2 * MID / BK_ : MID / BK_;   // phase-3 K-steps
   static constexpr int R3 = PROJ || MID > 64 ? 64 : 128; // output columns per phase-3 part
   static constexpr int NPART = CIO / R3;
@@ -225,16 +228,30 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
   const float sa = ldexpf(1.f, 15 - ex), inv0 = ldexpf(1.f, ex - 15);
   // row blocks wave and wave + 8 (the latter only for waves 0..3); lane fr's pixel of each
   const bool two = wave + NW < NRB1;                         // wave-uniform
-  unsigned av[2];
-  bool pv[2];                                                // that pixel is inside the image
+  // The x loads go out pixel-contiguous: load h (0, 1) of lane l reads pixel 8 h + (l >> 3) of
+  // the row block, 16-B chunk l & 7 of the K-step's 128 B (a lane quad = 64 contiguous bytes),
+  // and a wave-private 2-KiB slot per row block in TT (free until t1's epilogue) transposes them
+  // to the fragment layout (lane (fr, fg): pixel fr, channels fg*8 .. +7). Loaded straight into
+  // fragment lanes, every quad spanned 4 pixels 1 KB apart: the texture-address unit was busy
+  // 0.69 of the kernel's cycles after phase 3 went contiguous (profiles/r06_pmc_bneck_ta_ycoal.txt).
+  static_assert(NRB1 * 2048 <= S::TT_BYTES, "x transpose slots in TT");
+  unsigned av[2][2];
+  bool pv[2];                                                // pixel fr of row block i is inside the image
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int rb = wave + i * NW;
-    const int px = rb * 16 + fr;
-    const int hr = px / HW_, hc = px - hr * HW_;
-    const int ih = oh0 - 1 + hr, iw = ow0 - 1 + hc;
-    pv[i] = px < HP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && rb < NRB1;
-    av[i] = pv[i] ? (unsigned)(((int64_t)ih * p.xsh + (int64_t)iw * p.xsw + fg * 8) * 4) : BL_OOB;
+    auto inside = [&](int px, int& ih, int& iw) {
+      const int hr = px / HW_, hc = px - hr * HW_;
+      ih = oh0 - 1 + hr; iw = ow0 - 1 + hc;
+      return px < HP && (unsigned)ih < (unsigned)p.H && (unsigned)iw < (unsigned)p.W && rb < NRB1;
+    };
+    int ih, iw;
+    pv[i] = inside(rb * 16 + fr, ih, iw);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool v = inside(rb * 16 + 8 * h + (lane >> 3), ih, iw);
+      av[i][h] = v ? (unsigned)(((int64_t)ih * p.xsh + (int64_t)iw * p.xsw + (lane & 7) * 4) * 4) : BL_OOB;
+    }
   }
   f32x4 acc1[2][NJ1];
 #pragma unroll
@@ -242,22 +259,32 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
 #pragma unroll
     for (int j = 0; j < NJ1; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   // A straight from global into registers, two K-steps ahead (raw[step & 1])
-  f4 raw[2][2][2];
+  constexpr int AD = S::AD;
+  f4 raw[AD][2][2];
   auto load_a = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       if (i == 1 && !two) continue;
-      raw[kt & 1][i][0] = bl_f4(xr, av[i], kt * BK_ * 4);
-      raw[kt & 1][i][1] = bl_f4(xr, av[i] + 16, kt * BK_ * 4);
+      raw[kt % AD][i][0] = bl_f4(xr, av[i][0], kt * BK_ * 4);
+      raw[kt % AD][i][1] = bl_f4(xr, av[i][1], kt * BK_ * 4);
     }
   };
   f16x8 af[2][2];
   auto split = [&](int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
+      if (i == 1 && !two) continue;
+      // transpose through the row block's slot (chunk slots XOR-swizzled by pixel: the b128 reads
+      // of 8 lanes / 8 pixels hit 8 distinct bank quads); same-wave LDS ops complete in order
+      unsigned char* const scr = lds + (wave + i * NW) * 2048;
+      const int q0 = lane >> 3, c = lane & 7;
+      *reinterpret_cast<f4*>(scr + q0 * 128 + ((c ^ q0) << 4)) = raw[kt % AD][i][0];
+      *reinterpret_cast<f4*>(scr + (8 + q0) * 128 + ((c ^ q0) << 4)) = raw[kt % AD][i][1];
+      const f4 x0 = *reinterpret_cast<const f4*>(scr + fr * 128 + (((2 * fg) ^ (fr & 7)) << 4));
+      const f4 x1 = *reinterpret_cast<const f4*>(scr + fr * 128 + (((2 * fg + 1) ^ (fr & 7)) << 4));
       unsigned long long p0[2], p1[2];
-      split_planes_f16(raw[kt & 1][i][0], sa, p0);
-      split_planes_f16(raw[kt & 1][i][1], sa, p1);
+      split_planes_f16(x0, sa, p0);
+      split_planes_f16(x1, sa, p1);
 #pragma unroll
       for (int q = 0; q < 2; ++q) {
         typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -265,32 +292,51 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
       }
     }
   };
-  // Per step kt: [wait + barrier] W(kt + RING - 1), A(kt + 2) issued, MFMAs on A(kt), split of
-  // A(kt + 1). The wait leaves in flight exactly the ops issued after this wave's pieces of
-  // W(kt) (counted per step below: PPW pieces per W step, na = A loads per step), so A stays two
-  // steps ahead.
-  static_assert(RING == 4 && NK1 >= 2, "phase-1 wait counts");
+  // Per step kt: [wait + barrier] W(kt + RING - 1) issued, split of A(kt) (its registers are then
+  // free), A(kt + AD) issued into them, MFMAs on A(kt). A(kt) was issued AD steps earlier: the
+  // split waits for it at the start of its own step, not at the end of the one before (round 6:
+  // the phase timeline, tools/bneck_trace.py, had phase 1 at 42 % of a tile, ~2.4 us per K-step
+  // for ~0.3 us of MFMAs -- latency-bound on x with one step of cover). The wait leaves in flight
+  // exactly the ops issued after this wave's pieces of W(kt): 2 W steps (PPW pieces each) and
+  // na_step(kt) A steps (na = 4 / 2 loads each).
+  static_assert(RING == 4 && NK1 >= AD, "phase-1 wait counts");
 #pragma unroll
   for (int u = 0; u < RING - 1; ++u) issue_wu(u);
   // the counted waits below assume this issue order (W pieces, then the A loads); without the
   // fence the scheduler may hoist the A loads above the LDS-DMA (a build that only added A loads
   // did so, and W(0) was then not covered by the first wait: wrong results)
   __builtin_amdgcn_sched_barrier(0);
-  load_a(0);
-  load_a(1);
-  split(0);
+#pragma unroll
+  for (int k = 0; k < AD; ++k) load_a(k);
+  // A steps issued after W(kt): W(0..2) precede the AD prologue steps and steps 0..kt-1's loads;
+  // W(kt >= 3) is followed by the loads of steps kt-3..kt-1 (step j loads A(j + AD) if < NK1)
+  auto na_step = [&](int kt) {
+    int m = kt < RING - 1 ? AD : 0;
+    for (int j = kt < RING - 1 ? 0 : kt - (RING - 1); j < kt; ++j) m += j + AD < NK1;
+    return m;
+  };
 #pragma unroll
   for (int kt = 0; kt < NK1; ++kt) {
-    // ops issued after W(kt): kt = 0: W1, W2, A0, A1; middle steps: 2 W + 3 A steps (fewer only
-    // where the count is not needed: W(1), W(2) precede A(0)); last: 2 W + 2 A steps
+    const int m = na_step(kt);
     if (two) {
-      if (kt == 0 || kt == NK1 - 1) wait_barrier<2 * PPW + 2 * 4>(); else wait_barrier<2 * PPW + 3 * 4>();
+      if (m == 2) wait_barrier<2 * PPW + 2 * 4>();
+      else if (m == 3) wait_barrier<2 * PPW + 3 * 4>();
+      else if (m == 4) wait_barrier<2 * PPW + 4 * 4>();
+      else if (m == 5) wait_barrier<2 * PPW + 5 * 4>();
+      else if (m == 6) wait_barrier<2 * PPW + 6 * 4>();
+      else wait_barrier<2 * PPW>();                          // (m <= 1: a smaller count only waits longer)
     } else {
-      if (kt == 0 || kt == NK1 - 1) wait_barrier<2 * PPW + 2 * 2>(); else wait_barrier<2 * PPW + 3 * 2>();
+      if (m == 2) wait_barrier<2 * PPW + 2 * 2>();
+      else if (m == 3) wait_barrier<2 * PPW + 3 * 2>();
+      else if (m == 4) wait_barrier<2 * PPW + 4 * 2>();
+      else if (m == 5) wait_barrier<2 * PPW + 5 * 2>();
+      else if (m == 6) wait_barrier<2 * PPW + 6 * 2>();
+      else wait_barrier<2 * PPW>();
     }
     issue_wu(kt + RING - 1);
-    __builtin_amdgcn_sched_barrier(0);                       // W(kt + 3) before A(kt + 2): the counts
-    if (kt + 2 < NK1) load_a(kt + 2);
+    __builtin_amdgcn_sched_barrier(0);                       // W(kt + 3) before A(kt + AD): the counts
+    split(kt);
+    if (kt + AD < NK1) load_a(kt + AD);
     const unsigned char* sb = lds + RING_OFF + (kt % RING) * STAGE;
 #pragma unroll
     for (int j = 0; j < NJ1; ++j) {
@@ -299,7 +345,6 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
       acc1[0][j] = mfma3t(b, af[0], acc1[0][j]);
       if (two) acc1[1][j] = mfma3t(b, af[1], acc1[1][j]);
     }
-    if (kt + 1 < NK1) split(kt + 1);
   }
   // epilogue 1: bn1 + ReLU (zero outside the image: conv2's padding), tile max, planes -> TT.
   // Lane (fr, fg) holds channels j*16 + fg*4 .. +3 of pixel rb*16 + fr.
@@ -320,12 +365,15 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) m1 = fmaxf(m1, __shfl_xor(m1, o, 64));
-  wait_barrier<0>();                                         // every wave's phase-1 reads of the ring done
+  // every wave's phase-1 reads of the ring done (their MFMAs consumed them). The W2 steps
+  // W(NK1 .. NK1 + 2) issued in phase 1 stay in flight: a vmcnt(0) here made every tile wait for
+  // their landing before its t1 epilogue (round 6, tools/bneck_trace.py)
+  wait_barrier<(RING - 1) * PPW>();
   // tile max through per-wave slots in the ring stage of W1's last step (dead now; the next DMA
   // into it, W(NK1 + 3), is issued only after phase 2's first barrier): no zeroing, no atomics
   float* const wmax1 = reinterpret_cast<float*>(lds + RING_OFF + ((NK1 - 1) % RING) * STAGE);
   if (lane == 0) wmax1[wave] = m1;
-  __syncthreads();
+  lds_barrier();                                             // (not __syncthreads: its fence drains vmcnt)
   m1 = wmax1[0];
 #pragma unroll
   for (int w = 1; w < NW; ++w) m1 = fmaxf(m1, wmax1[w]);
@@ -402,9 +450,27 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
   float* const wmax2 = reinterpret_cast<float*>(lds + RING_OFF + 2 * STAGE);   // past the W3 overlay
   if (lane == 0) wmax2[wave] = m2;
   // PROJ: the downsample operand, x at this lane's output pixel (channels ks*32 + fg*8 .. +7),
-  // loaded now (older than every W3 piece, so the counted waits below stay exact)
+  // loaded now (older than every W3 piece, so the counted waits below stay exact).
+  // Identity: the residual of phase-3 part 0 (x at this lane's output pixel, channels j*16 +
+  // fg*4 .. +3), loaded now for the same reason: issued at part 0's start it was a full HBM
+  // latency behind the part's few MFMAs (round 6 phase timeline); part h + 1's is loaded by part
+  // h's epilogue as each column block frees its registers
   constexpr int NXK = PROJ ? MID / BK_ : 1;
+  constexpr int NJ3 = S::R3 / 16;
   f4 xc[NXK][2];
+  f4 res[PROJ ? 1 : NJ3];
+  // COAL: the residual loads and y stores go out pixel-contiguous (lane 4 q + c: pixel column q,
+  // channels c*4 .. +3 of a 16-channel block, so a lane quad covers 64 contiguous bytes) and the
+  // accumulator layout (lane = channels of pixel fr, quads spanning 4 pixels 1 KB apart) is
+  // transposed through a wave-private 1-KiB LDS slot in ring stage 2 (wmax2's stage, dead in
+  // phase 3). Round 6: TA_BUSY 0.76 of the kernel's cycles (profiles/r06_pmc_bneck_ta_base.txt) --
+  // address processing of the quad-scattered 16-B accesses, not HBM, set the kernel's pace.
+  constexpr bool COAL = NW * 1024 <= STAGE;
+  constexpr int SCR_OFF = RING_OFF + 2 * STAGE;
+  const int pxq = COAL ? (lane >> 2) : fr, chq = COAL ? (lane & 3) : fg;
+  const int oxq = ow0 + pxq;
+  const bool ovq = oy < p.H && oxq < p.W;
+  const unsigned rvo = ovq ? (unsigned)(((int64_t)oy * p.xsh + (int64_t)oxq * p.xsw + chq * 4) * 4) : BL_OOB;
   if constexpr (PROJ) {
     const unsigned cvo = ov ? (unsigned)(((int64_t)oy * p.xsh + (int64_t)ox * p.xsw + fg * 8) * 4) : BL_OOB;
 #pragma unroll
@@ -412,6 +478,9 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
       xc[ks][0] = bl_f4(xr, cvo, ks * BK_ * 4);
       xc[ks][1] = bl_f4(xr, cvo + 16, ks * BK_ * 4);
     }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NJ3; ++j) res[j] = bl_f4(xr, rvo, j * 16 * 4);
   }
   // W3 part h (R3 output columns, all NKS3 K-steps, both planes) into the overlay (TT past t2 +
   // ring stages 0-1; buffer h & 1 when double-buffered): 32 pieces, 4 per wave
@@ -449,7 +518,9 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
   asm volatile("" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
   issue_w3(0);
-  __syncthreads();
+  // an LDS-only barrier: __syncthreads' fence is a vmcnt(0), which made the t2 epilogue wait for
+  // W3 part 0 and part 0's residual; phase 3's first wait takes them instead, after this work
+  lds_barrier();
   m2 = wmax2[0];
 #pragma unroll
   for (int w = 1; w < NW; ++w) m2 = fmaxf(m2, wmax2[w]);
@@ -483,26 +554,21 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
   // (PROJ: y = relu(W' [t2 | x] + b3 + bd)). Residual loads and y stores are 16-B buffer
   // accesses (an invalid pixel's offset is past the descriptor: zeros / dropped), issued
   // unconditionally so every wave counts the same vmcnt.
-  constexpr int NPART = S::NPART, NKS3 = S::NKS3, NJ = R3 / 16;
+  constexpr int NPART = S::NPART, NKS3 = S::NKS3, NJ = NJ3;
   constexpr int NRES = PROJ ? 0 : NJ;                        // residual loads per part
   const int yframe_bytes = (int)(((int64_t)(p.H - 1) * p.ysh + (int64_t)(p.W - 1) * p.ysw + CIO) * 4);
   const __amdgpu_buffer_rsrc_t yr = buf_rsrc(p.y + (int64_t)n * p.ysn, yframe_bytes);
-  const unsigned rvo = ov ? (unsigned)(((int64_t)oy * p.xsh + (int64_t)ox * p.xsw + fg * 4) * 4) : BL_OOB;
-  const unsigned yvo = ov ? (unsigned)(((int64_t)oy * p.ysh + (int64_t)ox * p.ysw + fg * 4) * 4) : BL_OOB;
+  const unsigned yvo = ovq ? (unsigned)(((int64_t)oy * p.ysh + (int64_t)oxq * p.ysw + chq * 4) * 4) : BL_OOB;
   const int q3 = wave * 16 + fr;
   const int a3 = q3 * 128 + (((2 * fg) ^ swz_rows(q3)) << 4);
   float ymax = 0.f;
-  f4 res[PROJ ? 1 : NJ];
 #pragma unroll 1
   for (int h = 0; h < NPART; ++h) {
-    if constexpr (!PROJ) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) res[j] = bl_f4(xr, rvo, (h * R3 + j * 16) * 4);
-    }
     if (h == 0) {
-      wait_barrier<NRES>();                                  // t2 written (W3 part 0 landed at the __syncthreads)
+      wait_barrier<0>();                                     // t2 written; W3 part 0, SB3 and part 0's residual landed
     } else {
-      // W3 part h was issued before part h-1's NJ stores and this part's residual loads
+      // W3 part h was issued before part h-1's epilogue: its NJ stores and (identity) the NJ
+      // residual loads of this part
       wait_barrier<NJ + NRES>();
     }
     if constexpr (W3DB) {
@@ -542,27 +608,40 @@ __global__ __launch_bounds__(TRT * 64, (BShape<MIDT, PROJ, TRT>::WPC * TRT / 4))
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);             // (the counted waits assume this issue order)
     }
-    // (residual +) bn3 + ReLU: lane (fr, fg) = pixel (oy, ox), channels h*R3 + j*16 + fg*4 .. +3
+    // (residual +) bn3 + ReLU: lane (fr, fg) = pixel (oy, ox), channels h*R3 + j*16 + fg*4 .. +3;
+    // with COAL transposed to lane (pxq, chq) before the residual add
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int c0 = h * R3 + j * 16 + fg * 4;
       const float* const sb3 = reinterpret_cast<const float*>(lds + SB3_OFF);
       const f4 s = *reinterpret_cast<const f4*>(sb3 + c0), b = *reinterpret_cast<const f4*>(sb3 + CIO + c0);
+      f4 t;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) t[r] = fmaf(acc3[j][r] * inv2, s[r], b[r]);
+      if constexpr (COAL) {
+        // (swizzled chunk slots: the 8 lanes of each b128 access phase hit 8 distinct bank quads)
+        unsigned char* const scr = lds + SCR_OFF + wave * 1024;
+        *reinterpret_cast<f4*>(scr + fr * 64 + (((fg ^ (fr >> 2)) & 3) << 4)) = t;
+        t = *reinterpret_cast<const f4*>(scr + pxq * 64 + (((chq ^ (pxq >> 2)) & 3) << 4));
+      }
       f4 v;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float t = fmaf(acc3[j][r] * inv2, s[r], b[r]);
-        if constexpr (!PROJ) t += res[j][r];
-        v[r] = t > 0.f ? t : 0.f;
+        float u = t[r];
+        if constexpr (!PROJ) u += res[j][r];
+        v[r] = u > 0.f ? u : 0.f;
         ymax = fmaxf(ymax, v[r]);
       }
       bs_f4(yr, v, yvo, (h * R3 + j * 16) * 4);
       store_data_guard(v);
+      if constexpr (!PROJ) {
+        if (h + 1 < NPART) res[j] = bl_f4(xr, rvo, ((h + 1) * R3 + j * 16) * 4);
+      }
     }
     asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);             // (the counted waits assume this issue order)
   }
-  if (!ov) ymax = 0.f;                                       // (an invalid pixel's y is relu(bias))
+  if (!ovq) ymax = 0.f;                                      // (an invalid pixel's y is relu(bias))
   if (p.y_amax) amax_commit(p.y_amax + n, ymax);
 }
 
