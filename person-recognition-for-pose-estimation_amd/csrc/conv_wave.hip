@@ -68,7 +68,7 @@ constexpr int wave_wps() {
   return (NW == 8 && TM == 2 && NP == 2 && !PRO) || (NW == 4 && TM == 2 && ONE && KSF == 1 && !PRO) ? 4 : 2;
 }
 template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false,
-          bool APL = false, bool ONE = false, int KSF = 0>
+          bool APL = false, bool ONE = false, int KSF = 0, bool X11 = false>
 __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) void conv_wave_kernel(ConvK p) {
   static_assert(!APL || (NP == 2 && !F16 && !PRO && !DUAL), "planes input: two bf16 planes only");
   static_assert(!F16 || (NP == 2 && (!PRO || ONE)), "f16 planes: two planes, no prologue unless single-plane");
@@ -87,7 +87,21 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
   constexpr int CS = BN + 4;                          // epilogue row pitch (floats)
   constexpr int EPI = NW * 16 * CS * 4;
   constexpr int RING = STAGES * B_STAGE;
-  constexpr int LDS_BYTES = RING > EPI ? RING : EPI;
+  // X11 (1x1 convs without padding, two fp32-derived planes): the A loads go out pixel-contiguous
+  // -- load h (0, 1) of a row block: lane l reads row 8 h + (l >> 3), 16-B chunk l & 7 of the
+  // K-step's 128 B, so each lane quad covers 64 contiguous bytes -- and a wave-private 2-KiB LDS
+  // slot past the ring transposes them into the fragment layout (lane (fr, fg): row fr, channels
+  // 8 fg .. +7) before the split, one row block after the other. Straight into fragment lanes,
+  // every quad spans 4 pixels a row pitch apart: the texture-address unit was busy 0.68 of this
+  // kernel's cycles over the model (profiles/r06_pmc_ta_table.txt). In the model (same box,
+  // profiles/r06_layer_profile_x11_ab.txt) the trunk's 1x1 convs ran 2-10 % faster this way and
+  // its 3x3 convs 2-6 % slower (their tap masks and more LDS traffic per MFMA), so the launcher
+  // picks X11 for 1x1 convs only.
+  constexpr bool XC = X11;
+  static_assert(!X11 || (!PRO && !APL && NP == 2 && !ONE), "pixel-contiguous A: two-plane forms, no prologue");
+  constexpr int XC_OFF = RING;
+  constexpr int MAIN = RING + (XC ? NW * 2048 : 0);
+  constexpr int LDS_BYTES = MAIN > EPI ? MAIN : EPI;
   static_assert(STAGES == 2 || STAGES == 3, "stages");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[LDS_BYTES];
 
@@ -161,6 +175,37 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
     hmask[i] = hm;
     wmask[i] = wmk;
   }
+  // XC: the rows this lane loads are row 8 h + (lane >> 3) of row block i, chunk lane & 7. x is
+  // dense and the conv 1x1 / stride 1 (the launcher's condition), so row m sits at m xsw floats:
+  // one lane offset from a descriptor based at the wave's first row, the (i, h) row step in the
+  // scalar offset, rows past M beyond the descriptor's range (zeros). x2 (a dual GEMM's strided
+  // second input) keeps per-row offsets.
+  __amdgpu_buffer_rsrc_t xlr = xr;
+  unsigned xlv = 0;
+  const int xsw4 = (int)(p.xsw * 4);
+  if constexpr (XC) {
+    const int64_t nrec = ((int64_t)(p.M - wrow0 - 1) * p.xsw + p.Ci) * 4;
+    xlr = buf_rsrc(p.x + (int64_t)wrow0 * p.xsw, (int)(nrec < 0 ? 0 : nrec < 0x7FFFFFF0 ? nrec : 0x7FFFFFF0));
+    xlv = (unsigned)(((lane >> 3) * (int)p.xsw + (lane & 7) * 4) * 4);
+  }
+  unsigned rv2c[XC && DUAL ? TM : 1][2];
+  if constexpr (XC && DUAL) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = wrow0 + i * 16 + 8 * h + (lane >> 3);
+        unsigned v2 = BL_OOB;
+        if (m < p.M) {
+          const int n = m / p.HoWo;
+          const int rem = m - n * p.HoWo;
+          const int oh = rem / p.Wo;
+          const int ow = rem - oh * p.Wo;
+          v2 = (unsigned)(((int64_t)(n - nf0) * p.x2sn + (int64_t)oh * p.x2sh + (int64_t)ow * p.x2sw + (lane & 7) * 4) * 4);
+        }
+        rv2c[i][h] = v2;
+      }
+  }
 
   // ---- B pieces: piece j -> plane j / (BN/16), rows 16 (j % (BN/16)) .. +16; lane -> (row, slot),
   // through one descriptor per plane (the K-step's 64 B as soffset)
@@ -220,7 +265,19 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const bool ok = (hmask[i] >> u_kh) & (wmask[i] >> u_kw) & 1u;
-      if constexpr (DUAL) {
+      if constexpr (XC && DUAL) {
+        if (second) {                                   // x2: 1x1, never padded
+          const int so = (u_off - p.nk1 * BK) * 4;
+          raw[ks][i][0] = bl_f4(x2r, rv2c[i][0], so);
+          raw[ks][i][1] = bl_f4(x2r, rv2c[i][1], so);
+        } else {
+          raw[ks][i][0] = bl_f4(xlr, xlv, u_off * 4 + 16 * i * xsw4);
+          raw[ks][i][1] = bl_f4(xlr, xlv, u_off * 4 + (16 * i + 8) * xsw4);
+        }
+      } else if constexpr (XC) {
+        raw[ks][i][0] = bl_f4(xlr, xlv, u_off * 4 + 16 * i * xsw4);
+        raw[ks][i][1] = bl_f4(xlr, xlv, u_off * 4 + (16 * i + 8) * xsw4);
+      } else if constexpr (DUAL) {
         if (second) {                                   // x2: 1x1, never padded
           const int so = (u_off - p.nk1 * BK) * 4;
           raw[ks][i][0] = bl_f4(x2r, rv2[i], so);
@@ -255,6 +312,16 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
 #pragma unroll
      for (int ks = 0; ks < KS; ++ks) {
       f4 v0 = raw[ks][i][0], v1 = raw[ks][i][1];
+      if constexpr (XC) {
+        // transpose through this wave's slot (chunk slots XOR-swizzled by row: the b128 reads of
+        // 8 lanes / 8 rows hit 8 distinct bank quads); same-wave LDS ops complete in order
+        unsigned char* const scr = lds + XC_OFF + wave * 2048;
+        const int q0 = lane >> 3, c = lane & 7;
+        *reinterpret_cast<f4*>(scr + q0 * 128 + ((c ^ q0) << 4)) = v0;
+        *reinterpret_cast<f4*>(scr + (8 + q0) * 128 + ((c ^ q0) << 4)) = v1;
+        v0 = *reinterpret_cast<const f4*>(scr + fr * 128 + (((2 * fg) ^ (fr & 7)) << 4));
+        v1 = *reinterpret_cast<const f4*>(scr + fr * 128 + (((2 * fg + 1) ^ (fr & 7)) << 4));
+      }
       if constexpr (PRO) {
         if constexpr (ONE) {                          // (as conv_halo.hip's precision-4 prologue)
           v0 = affine4(v0, as4[ks][0], ab4[ks][0]);
@@ -288,6 +355,7 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
           af[q][i] = bf16x8{p0[q][0], p0[q][1], p0[q][2], p0[q][3], p1[q][0], p1[q][1], p1[q][2], p1[q][3]};
       }
      }
+     if constexpr (XC) __builtin_amdgcn_sched_barrier(0);   // one row block's transpose live at a time
     }
   };
 
@@ -489,11 +557,21 @@ int launch(const ConvK& kp0, hipStream_t st) {
                          dim3(NW * 64), 0, st, kp);
     return launch_status();
   }
+  // 1x1, stride 1, no padding, dense x: the pixel-contiguous A loads (X11, two planes only)
+  const bool x11 = NP == 2 && kp.KH == 1 && kp.KW == 1 && kp.pad == 0 && kp.stride == 1 &&
+                   kp.xsh == (int64_t)kp.Wi * kp.xsw && kp.xsn == (int64_t)kp.Hi * kp.xsh && kp.xsw >= kp.Ci;
   if (kp.x2) {
-    if constexpr (F16)
-      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
-    else
+    // (not the dual precision-3 256 x 128 tile: its x2 row offsets stay per lane and spilled it)
+    constexpr bool dual_x11 = !(NW == 8 && TM == 2 && TN == 8 && STAGES == 3);
+    if constexpr (F16) {
+      if (x11 && dual_x11)
+        hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, true, false, false, 0, dual_x11>),
+                           dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+      else
+        hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+    } else {
       hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, false, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+    }
     return launch_status();
   }
   if (kp.x_planes) {
@@ -502,12 +580,23 @@ int launch(const ConvK& kp0, hipStream_t st) {
                             dim3(NW * 64), 0, st, kp);
     return launch_status();
   }
-  if constexpr (F16)
-    hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
-  else if (kp.in_scale)
+  if constexpr (F16) {
+    if (x11)
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, false, false, false, 0, true>),
+                         dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+    else
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  } else if (kp.in_scale)
     hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
-  else
+  else if constexpr (NP == 2) {
+    if (x11)
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, false, false, false, false, 0, true>),
+                         dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+    else
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  } else {
     hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+  }
   return launch_status();
 }
 

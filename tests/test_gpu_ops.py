@@ -272,6 +272,37 @@ def test_conv_wave_kernel_bit_exact_vs_lds_staged(B, Ci, H, W, Co, k, s, p, tile
     torch.testing.assert_close(got, ref, rtol=0, atol=_tol(x, w) * 2)
 
 
+@pytest.mark.parametrize("precision,tile", [(3, 23), (3, 25), (3, 26), (3, 27), (0, 23), (0, 28)])
+@pytest.mark.parametrize("B,H,W,Ci,Co", [(2, 17, 19, 64, 96), (3, 11, 13, 256, 256), (1, 40, 40, 128, 512)])
+def test_conv_wave_pixel_contiguous_1x1_bit_exact(B, H, W, Ci, Co, precision, tile):
+    """1x1 / stride-1 convs over a dense input take conv_wave's pixel-contiguous A path (X11: lane
+    quads on 64 contiguous bytes, transposed to the fragment layout through LDS, rows past M
+    beyond the descriptor); the same conv over a cropped view of a larger buffer (not dense)
+    takes the fragment-lane loads. Bit-identical (ragged M tails and a pre-activation residual
+    included), and both at the fp64 reference's tolerance."""
+    x = (torch.rand(B, H, W, Ci, generator=_g(90)) * 2 - 1).to(DEV)
+    big = torch.zeros(B, H + 2, W + 3, Ci, device=DEV)
+    big[:, 1:H + 1, 2:W + 2] = x
+    xv = big[:, 1:H + 1, 2:W + 2]
+    w = rnd(Co, Ci, 1, 1, seed=91, scale=1.0 / math.sqrt(Ci))
+    sc = torch.rand(Co, generator=_g(92)) + 0.5
+    bi = rnd(Co, seed=93)
+    pk = pack.pack_conv("t", w, 1, 0, DEV, scale=sc, bias=bi, act="relu")
+    r = (torch.rand(B, H, W, Co, generator=_g(94)) - 0.5).to(DEV)
+    xa = x.abs().flatten(1).amax(1).contiguous()
+    outs = []
+    for xin in (x, xv):
+        y = torch.empty(B, H, W, Co, device=DEV)
+        ops.conv2d(xin, pk, y, res=r, res_mode=RES_PRE, precision=precision, tile=tile,
+                   x_amax=xa if precision == 3 else None)
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = ref_conv(x.permute(0, 3, 1, 2).cpu(), w, 1, 0, act="relu", scale=sc, bias=bi,
+                   res=r.permute(0, 3, 1, 2).cpu(), res_mode=RES_PRE)
+    torch.testing.assert_close(outs[0].permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=_tol(x, w) * 2)
+
+
 @pytest.mark.parametrize("precision,tile", [(0, 28), (0, 29), (2, 27)])
 @pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", WAVE_SHAPES)
 def test_conv_wave_two_stage_ring_bit_exact(B, Ci, H, W, Co, k, s, p, tile, precision):
