@@ -206,15 +206,17 @@ def test_occupancy_critical_tiles_fit_128_vgprs_without_spills(asm_dir):
     # planes-input variants alike) and NW 4, TM 2, single-plane (ONE) with KSF 1, no prologue
     meta = _kernel_meta([o for o in asm_dir if o.endswith("conv_wave.s")][0])
 
-    def targs(name):   # NW, TM, TN, NP, STAGES, PRO, F16, DUAL, APL, ONE, KSF from the mangled name
+    def targs(name):   # NW, TM, TN, NP, STAGES, PRO, F16, DUAL, APL, ONE, KSF, X11 from the mangled name
         m = re.search(r"conv_wave_kernelI((?:L[ib]n?\d+E)+)E", name)
         return [int(v.replace("n", "-")) for v in re.findall(r"L[ib](n?\d+)E", m.group(1))] if m else None
 
     def wps4(a):
-        nw, tm, _tn, np_, _st, pro, _f16, _dual, _apl, one, ksf = a
+        nw, tm, _tn, np_, _st, pro, _f16, _dual, _apl, one, ksf, _x11 = a
         return (nw == 8 and tm == 2 and np_ == 2 and not pro) or (nw == 4 and tm == 2 and one and ksf == 1 and not pro)
 
-    hot = {k: v for k, v in meta.items() if targs(k) and len(targs(k)) == 11 and wps4(targs(k))}
+    hot = {k: v for k, v in meta.items() if targs(k) and len(targs(k)) == 12 and wps4(targs(k))}
+    # (the pixel-contiguous 1x1 forms, X11, included: same launch bound)
+    assert any(targs(k)[11] for k in hot), sorted(hot)
     assert any("conv_wave_kernelILi8ELi2ELi8ELi2ELi3ELb0ELb1E" in k for k in hot), sorted(meta)   # p3 256x128
     assert any("conv_wave_kernelILi4ELi2ELi8ELi2ELi2ELb0ELb1ELb0ELb0ELb1ELi1E" in k for k in hot)   # p4, KSF 1
     assert len(hot) >= 4, sorted(hot)
