@@ -68,7 +68,7 @@ constexpr int wave_wps() {
   return (NW == 8 && TM == 2 && NP == 2 && !PRO) || (NW == 4 && TM == 2 && ONE && KSF == 1 && !PRO) ? 4 : 2;
 }
 template <int NW, int TM, int TN, int NP, int STAGES, bool PRO, bool F16 = false, bool DUAL = false,
-          bool APL = false, bool ONE = false, int KSF = 0, bool X11 = false>
+          bool APL = false, bool ONE = false, int KSF = 0, int XM = 0>
 __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) void conv_wave_kernel(ConvK p) {
   static_assert(!APL || (NP == 2 && !F16 && !PRO && !DUAL), "planes input: two bf16 planes only");
   static_assert(!F16 || (NP == 2 && (!PRO || ONE)), "f16 planes: two planes, no prologue unless single-plane");
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
   constexpr int CS = BN + 4;                          // epilogue row pitch (floats)
   constexpr int EPI = NW * 16 * CS * 4;
   constexpr int RING = STAGES * B_STAGE;
-  // X11 (1x1 convs without padding, two fp32-derived planes): the A loads go out pixel-contiguous
+  // XM 1 (1x1 convs without padding, two fp32-derived planes): the A loads go out pixel-contiguous
   // -- load h (0, 1) of a row block: lane l reads row 8 h + (l >> 3), 16-B chunk l & 7 of the
   // K-step's 128 B, so each lane quad covers 64 contiguous bytes -- and a wave-private 2-KiB LDS
   // slot past the ring transposes them into the fragment layout (lane (fr, fg): row fr, channels
@@ -96,9 +96,12 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
   // kernel's cycles over the model (profiles/r06_pmc_ta_table.txt). In the model (same box,
   // profiles/r06_layer_profile_x11_ab.txt) the trunk's 1x1 convs ran 2-10 % faster this way and
   // its 3x3 convs 2-6 % slower (their tap masks and more LDS traffic per MFMA), so the launcher
-  // picks X11 for 1x1 convs only.
-  constexpr bool XC = X11;
-  static_assert(!X11 || (!PRO && !APL && NP == 2 && !ONE), "pixel-contiguous A: two-plane forms, no prologue");
+  // picks them for 1x1 convs (XM 1) and for unpadded convs of any size (XM 2: per-lane row
+  // offsets, no tap masks -- the trunk's 3x3 convs read a zero-bordered copy of their input with
+  // pad 0, engine.py, so they carry no masks either; with masks the 256 x 128 tile spilled).
+  constexpr bool XC = XM != 0, XLIN = XM == 1;
+  static_assert(!XC || (!PRO && !APL && NP == 2 && !ONE), "pixel-contiguous A: two-plane forms, no prologue");
+  static_assert(XM != 2 || !DUAL, "dual GEMMs are 1x1 (XM 1)");
   constexpr int XC_OFF = RING;
   constexpr int MAIN = RING + (XC ? NW * 2048 : 0);
   constexpr int LDS_BYTES = MAIN > EPI ? MAIN : EPI;
@@ -183,12 +186,32 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
   __amdgpu_buffer_rsrc_t xlr = xr;
   unsigned xlv = 0;
   const int xsw4 = (int)(p.xsw * 4);
-  if constexpr (XC) {
+  if constexpr (XLIN) {
     const int64_t nrec = ((int64_t)(p.M - wrow0 - 1) * p.xsw + p.Ci) * 4;
     xlr = buf_rsrc(p.x + (int64_t)wrow0 * p.xsw, (int)(nrec < 0 ? 0 : nrec < 0x7FFFFFF0 ? nrec : 0x7FFFFFF0));
     xlv = (unsigned)(((lane >> 3) * (int)p.xsw + (lane & 7) * 4) * 4);
   }
   unsigned rv2c[XC && DUAL ? TM : 1][2];
+  // XM 2: per-lane offsets of tap (0, 0) of those rows (the tap and chunk are the soffset)
+  unsigned rvp[XM == 2 ? TM : 1][2];
+  if constexpr (XM == 2) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = wrow0 + i * 16 + 8 * h + (lane >> 3);
+        unsigned v = BL_OOB;
+        if (m < p.M) {
+          const int n = m / p.HoWo;
+          const int rem = m - n * p.HoWo;
+          const int oh = rem / p.Wo;
+          const int ow = rem - oh * p.Wo;
+          v = (unsigned)(((int64_t)(n - nf0) * p.xsn + (int64_t)oh * p.stride * p.xsh +
+                          (int64_t)ow * p.stride * p.xsw + (lane & 7) * 4) * 4);
+        }
+        rvp[i][h] = v;
+      }
+  }
   if constexpr (XC && DUAL) {
 #pragma unroll
     for (int i = 0; i < TM; ++i)
@@ -274,9 +297,12 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
           raw[ks][i][0] = bl_f4(xlr, xlv, u_off * 4 + 16 * i * xsw4);
           raw[ks][i][1] = bl_f4(xlr, xlv, u_off * 4 + (16 * i + 8) * xsw4);
         }
-      } else if constexpr (XC) {
+      } else if constexpr (XLIN) {
         raw[ks][i][0] = bl_f4(xlr, xlv, u_off * 4 + 16 * i * xsw4);
         raw[ks][i][1] = bl_f4(xlr, xlv, u_off * 4 + (16 * i + 8) * xsw4);
+      } else if constexpr (XM == 2) {
+        raw[ks][i][0] = bl_f4(xr, rvp[i][0], u_off * 4);
+        raw[ks][i][1] = bl_f4(xr, rvp[i][1], u_off * 4);
       } else if constexpr (DUAL) {
         if (second) {                                   // x2: 1x1, never padded
           const int so = (u_off - p.nk1 * BK) * 4;
@@ -339,8 +365,14 @@ __global__ __launch_bounds__(NW * 64, (wave_wps<NW, TM, NP, PRO, ONE, KSF>())) v
         af[ks][i] = cvt_f16_one(v0, v1, sa[i]);
       } else if constexpr (F16) {
         unsigned long long p0[2], p1[2];
-        split_planes_f16(v0, sa[i], p0);
-        split_planes_f16(v1, sa[i], p1);
+        // XM 2 (launched only when a frame holds >= WTM rows: "two") takes the row's scale from the
+        // two frames' wave-uniform scales instead of a register per row: the 256 x 128 tile sits
+        // at its 128-VGPR cap and the per-lane offsets of XM 2 needed those registers
+        float s_i = sa[i];
+        if constexpr (XM == 2)
+          s_i = wrow0 + i * 16 + fr >= nb ? ldexpf(1.f, 15 - f16_scale_exp(am1)) : ldexpf(1.f, 15 - f16_scale_exp(am0));
+        split_planes_f16(v0, s_i, p0);
+        split_planes_f16(v1, s_i, p1);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
           typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
@@ -557,15 +589,17 @@ int launch(const ConvK& kp0, hipStream_t st) {
                          dim3(NW * 64), 0, st, kp);
     return launch_status();
   }
-  // 1x1, stride 1, no padding, dense x: the pixel-contiguous A loads (X11, two planes only)
+  // the pixel-contiguous A loads (two planes only): XM 1 for 1x1 / stride-1 convs over a dense
+  // x (linear row addressing), XM 2 for any other unpadded conv (per-lane row offsets)
   const bool x11 = NP == 2 && kp.KH == 1 && kp.KW == 1 && kp.pad == 0 && kp.stride == 1 &&
                    kp.xsh == (int64_t)kp.Wi * kp.xsw && kp.xsn == (int64_t)kp.Hi * kp.xsh && kp.xsw >= kp.Ci;
+  const bool xp0 = NP == 2 && kp.pad == 0 && !x11 && kp.Ho * kp.Wo >= TM * 16;
   if (kp.x2) {
     // (not the dual precision-3 256 x 128 tile: its x2 row offsets stay per lane and spilled it)
     constexpr bool dual_x11 = !(NW == 8 && TM == 2 && TN == 8 && STAGES == 3);
     if constexpr (F16) {
       if (x11 && dual_x11)
-        hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, true, false, false, 0, dual_x11>),
+        hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, true, false, false, 0, dual_x11 ? 1 : 0>),
                            dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
       else
         hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
@@ -582,7 +616,10 @@ int launch(const ConvK& kp0, hipStream_t st) {
   }
   if constexpr (F16) {
     if (x11)
-      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, false, false, false, 0, true>),
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, false, false, false, 0, 1>),
+                         dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+    else if (xp0)
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true, false, false, false, 0, 2>),
                          dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
     else
       hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
@@ -590,7 +627,10 @@ int launch(const ConvK& kp0, hipStream_t st) {
     hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, NP, STAGES, true>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
   else if constexpr (NP == 2) {
     if (x11)
-      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, false, false, false, false, 0, true>),
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, false, false, false, false, 0, 1>),
+                         dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
+    else if (xp0)
+      hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false, false, false, false, false, 0, 2>),
                          dim3(kp.nwg), dim3(NW * 64), 0, st, kp);
     else
       hipLaunchKernelGGL((conv_wave_kernel<NW, TM, TN, 2, STAGES, false>), dim3(kp.nwg), dim3(NW * 64), 0, st, kp);

@@ -87,6 +87,10 @@ STEM_POOL = os.environ.get("PRPE_STEM_POOL", "1") != "0"
 # of a zero-bordered NHWC4 copy of the crops, as the stem (Engine.vit_pix4); PRPE_VIT_PATCH_VIEW=0
 # runs the plain 16x16 conv on the 3-channel crops (the gather-bound small-Ci kernel)
 PATCH_VIEW = os.environ.get("PRPE_VIT_PATCH_VIEW", "1") != "0"
+# the unfused trunk blocks' 3x3 conv2 over a zero-bordered copy of its input, unpadded (no tap
+# masks: conv_wave's pixel-contiguous A loads; Engine.bordered); PRPE_T1_BORDER=0 runs it with
+# pad 1 on the plain conv1 output
+T1_BORDER = os.environ.get("PRPE_T1_BORDER", "1") != "0"
 
 
 class _Prec:
@@ -137,6 +141,16 @@ class Engine:
     # ------------------------------------------------------------------ helpers
     def empty(self, *shape):
         return torch.empty(*shape, device=self.device, dtype=torch.float32)
+
+    def bordered(self, B, H, W, C):
+        """A [B, H+2, W+2, C] buffer whose one-pixel border is zero (allocated zeroed once per
+        shape; only its interior is ever written): the input of an unpadded 3x3 conv."""
+        key = ("bordered", B, H, W, C)
+        t = self._aux.get(key)
+        if t is None:
+            t = torch.zeros(B, H + 2, W + 2, C, device=self.device, dtype=torch.float32)
+            self._aux[key] = t
+        return t
 
     def dev(self, key, fn=None):
         t = self._aux.get(key)
@@ -421,8 +435,20 @@ class Engine:
                 if b == 0 and s == 1 and self._bneck_ok(x, planes, proj=True):
                     x = self.bottleneck(q, x, proj=True)
                     continue
-                o = self.conv(x, self.pk(q + ".conv1", q + ".conv1.weight", bn=q + ".bn1", act="relu"))
-                o = self.conv(o, self.pk(q + ".conv2", q + ".conv2.weight", s, 1, bn=q + ".bn2", act="relu"))
+                p1 = self.pk(q + ".conv1", q + ".conv1.weight", bn=q + ".bn1", act="relu")
+                if T1_BORDER:
+                    # conv1 writes the interior of a zero-bordered buffer and the 3x3 conv2 reads
+                    # all of it unpadded (pad 0): same sums (a padded tap adds 0 either way), and
+                    # the conv has no tap masks, so it takes conv_wave's pixel-contiguous A loads
+                    # (XM 2; csrc/conv_wave.hip)
+                    B_, H_, W_, _ = x.shape
+                    tb = self.bordered(B_, H_, W_, p1.co)
+                    o = self.conv(x, p1, out=tb[:, 1:H_ + 1, 1:W_ + 1, :])
+                    tb._prpe_amax = o._prpe_amax                  # the zero border never raises max|x|
+                    o = self.conv(tb, self.pk(q + ".conv2", q + ".conv2.weight", s, 0, bn=q + ".bn2", act="relu"))
+                else:
+                    o = self.conv(x, p1)
+                    o = self.conv(o, self.pk(q + ".conv2", q + ".conv2.weight", s, 1, bn=q + ".bn2", act="relu"))
                 if b == 0:
                     # conv3 + bn3 and the downsample projection + its BN summed in one dual-input
                     # GEMM: the projection never goes to HBM as a residual tensor

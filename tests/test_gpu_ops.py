@@ -303,6 +303,33 @@ def test_conv_wave_pixel_contiguous_1x1_bit_exact(B, H, W, Ci, Co, precision, ti
     torch.testing.assert_close(outs[0].permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=_tol(x, w) * 2)
 
 
+@pytest.mark.parametrize("precision,tile", [(3, 23), (3, 25), (3, 27), (0, 23), (0, 28)])
+@pytest.mark.parametrize("B,H,W,Ci,Co,s", [(2, 17, 19, 64, 96, 1), (3, 12, 10, 128, 256, 1), (2, 20, 20, 256, 256, 2),
+                                           (1, 40, 40, 64, 128, 1)])
+def test_conv_wave_unpadded_over_zero_border_bit_exact(B, H, W, Ci, Co, s, precision, tile):
+    """The trunk's 3x3 conv2 over a zero-bordered copy of its input with pad 0 (engine
+    T1_BORDER: no tap masks, conv_wave's pixel-contiguous A loads, XM 2) equals the pad-1 conv
+    over the plain input (fragment-lane loads with tap masks) bit for bit, stride 2 included."""
+    x = (torch.rand(B, H, W, Ci, generator=_g(95)) * 2 - 1).to(DEV)
+    xb = torch.zeros(B, H + 2, W + 2, Ci, device=DEV)
+    xb[:, 1:H + 1, 1:W + 1] = x
+    w = rnd(Co, Ci, 3, 3, seed=96, scale=1.0 / math.sqrt(Ci * 9))
+    sc = torch.rand(Co, generator=_g(97)) + 0.5
+    bi = rnd(Co, seed=98)
+    xa = x.abs().flatten(1).amax(1).contiguous()
+    outs = []
+    for xin, pad in ((x, 1), (xb, 0)):
+        pk = pack.pack_conv("t", w, s, pad, DEV, scale=sc, bias=bi, act="relu", k_order=1)
+        Ho, Wo = (H + 2 - 3) // s + 1, (W + 2 - 3) // s + 1
+        y = torch.empty(B, Ho, Wo, Co, device=DEV)
+        ops.conv2d(xin, pk, y, precision=precision, tile=tile, x_amax=xa if precision == 3 else None)
+        outs.append(y)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = ref_conv(x.permute(0, 3, 1, 2).cpu(), w, s, 1, act="relu", scale=sc, bias=bi)
+    torch.testing.assert_close(outs[1].permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=_tol(x, w) * 2)
+
+
 @pytest.mark.parametrize("precision,tile", [(0, 28), (0, 29), (2, 27)])
 @pytest.mark.parametrize("B,Ci,H,W,Co,k,s,p", WAVE_SHAPES)
 def test_conv_wave_two_stage_ring_bit_exact(B, Ci, H, W, Co, k, s, p, tile, precision):
