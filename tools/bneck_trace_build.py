@@ -52,8 +52,8 @@ EDITS = [
     ("  // epilogue 2: bn2 + ReLU", "  const unsigned long long T2 = __builtin_amdgcn_s_memrealtime();\n  // epilogue 2: bn2 + ReLU"),
     ("  // =========================== phase 3: y",
      "  const unsigned long long T2b = __builtin_amdgcn_s_memrealtime();\n  // =========================== phase 3: y"),
-    ("  if (!ov) ymax = 0.f;                                       // (an invalid pixel's y is relu(bias))\n",
-     "  if (!ov) ymax = 0.f;                                       // (an invalid pixel's y is relu(bias))\n"
+    ("  if (!ovq) ymax = 0.f;                                      // (an invalid pixel's y is relu(bias))\n",
+     "  if (!ovq) ymax = 0.f;                                      // (an invalid pixel's y is relu(bias))\n"
      "  {\n    const unsigned long long T3 = __builtin_amdgcn_s_memrealtime();\n"
      "    unsigned hw, xcc;\n"
      "    asm volatile(\"s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\" : \"=s\"(hw));\n"
